@@ -1,0 +1,221 @@
+/*
+ * mochi_hip.h — C ABI of libmochi_hip, the MI355X batch verifier for MochiDB's
+ * Write2 certificate path.
+ *
+ * What this replaces in the reference (tomisetsu/mochi-db, Java):
+ *
+ *   InMemoryDataStore.processWrite2ToServer(Write2ToServer)           InMemoryDataStore.java:641-666
+ *     ├ processMultiGrantsFromAllServers(wc.grantsMap, txn)           InMemoryDataStore.java:613-640
+ *     └ write2apply(coalesced, msg)  (verdict part only)              InMemoryDataStore.java:576-611
+ *   ClusterConfiguration.getServerMajority()                          ClusterConfiguration.java:264-267
+ *   MochiDBClient Write2/Read response aggregation                    MochiDBClient.java:148-175, 355-382
+ *
+ * plus the per-grant signature check the reference leaves as a TODO
+ * (MochiProtocol.proto:123 "// TODO: add signature"): SHA-256 over the
+ * proto3-encoded Grant (MochiProtocol.java:7556-7574) and an RSA-2048
+ * PKCS#1 v1.5 verify (JCA "SHA256withRSA", e = 65537).
+ *
+ * ABI rules: plain C, plain pointers and sizes, no torch / HIP types in the
+ * signatures (a hipStream_t travels as void*).  Every entry point returns an
+ * int status: 0 = ok, < 0 = argument / HIP error (text in mochi_last_error()).
+ * A verdict is NEVER an error: rejects are bits and reason codes in the
+ * output buffers (the reference throws, and RequestHandlerDispatcher.java:74-79
+ * swallows, so a reject is observable only as a missing Write2Ans; the Java
+ * shim in INTEGRATION.md maps reason codes back to those exception types).
+ */
+#ifndef MOCHI_HIP_H
+#define MOCHI_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MOCHI_ABI_VERSION 1
+#define MOCHI_RSA_BYTES 256     /* RSA-2048 modulus / signature size            */
+#define MOCHI_RSA_E 65537u      /* the only public exponent supported          */
+#define MOCHI_TXN_HASH_BYTES 128 /* lowercase-hex SHA-512 (Utils.java:135-153)  */
+#define MOCHI_MAX_KEYS 4096     /* key-table entries per context               */
+#define MOCHI_MAX_OPS_PER_CERT 64 /* transaction operations per certificate    */
+
+/* Status codes. */
+#define MOCHI_OK 0
+#define MOCHI_EINVAL (-1)  /* bad argument / inconsistent batch          */
+#define MOCHI_EHIP (-2)    /* HIP runtime error                          */
+#define MOCHI_ENOMEM (-3)  /* device or pinned-host allocation failed    */
+#define MOCHI_ENODEV (-4)  /* no usable gfx950 device                    */
+
+/* Per-certificate verdict reason codes.  Each maps to the exception the
+ * reference throws on that branch (see INTEGRATION.md for the Java mapping). */
+enum mochi_reason {
+  MOCHI_ACCEPT = 0,
+  /* processMultiGrantsFromAllServers: a valid grant's timestamp differs from the
+   * first valid grant seen for the same key -> UnsupportedOperationException
+   * (InMemoryDataStore.java:626-628). */
+  MOCHI_REJECT_TS_MISMATCH = 1,
+  /* write2apply: no valid grant for a local op's key -> coalescedTxnGrantMap.get()
+   * returns null -> NullPointerException (InMemoryDataStore.java:588). */
+  MOCHI_REJECT_NO_GRANT = 2,
+  /* write2apply: list.size() > getServerMajority() fails -> IllegalStateException
+   * via Utils.assertTrue (InMemoryDataStore.java:590, Utils.java:43-47).  With
+   * strict_gt = 0 the client predicate ">=" (MochiDBClient.java:172,379) is used. */
+  MOCHI_REJECT_BELOW_QUORUM = 3,
+  /* write2apply: g0.transactionHash != objectSHA512(txn) ->
+   * UnsupportedOperationException (InMemoryDataStore.java:591,605-607). */
+  MOCHI_REJECT_HASH_MISMATCH = 4,
+  /* write2apply: no StoreValueObjectContainer for the key -> NullPointerException
+   * (InMemoryDataStore.java:592-593).  Driven by MOCHI_OP_HAS_SVOC. */
+  MOCHI_REJECT_NO_SVOC = 5,
+  /* a grant's bytes are not a parseable proto3 Grant (the reference would fail
+   * in the Netty protobuf decoder, MochiServerInitializer.java:30-34). */
+  MOCHI_REJECT_MALFORMED = 6,
+};
+
+/* op_flags bits (one byte per transaction operation). */
+#define MOCHI_OP_LOCAL 0x01    /* objectBelongsToCurrentShardServer(key)      InMemoryDataStore.java:63-72,582 */
+#define MOCHI_OP_HAS_SVOC 0x02 /* getDataMap(key).get(key) != null           InMemoryDataStore.java:592 */
+
+/* grant_flags bits (one byte per grant, output). */
+#define MOCHI_GRANT_SIG_OK 0x01   /* RSA/SHA-256 signature verified            */
+#define MOCHI_GRANT_PARSED 0x02   /* bytes parsed as a Grant                   */
+
+/*
+ * A batch of Write2 certificates in struct-of-arrays form.
+ *
+ * Grants are listed certificate by certificate, in certificate WIRE order
+ * (the MultiGrant map iteration order, which decides which grant is "g0",
+ * InMemoryDataStore.java:588, MochiDBClient.java:333-338).  A grant's bytes
+ * are the exact proto3 encoding that was signed (Grant.toByteArray(),
+ * MochiProtocol.java:7556-7574) and may sit anywhere in `grant_bytes`
+ * (e.g. as slices of the received Write2ToServer wire buffer: zero copy).
+ *
+ * All arrays are host pointers for mochi_verify_batch() and device pointers
+ * for mochi_verify_batch_device().
+ */
+typedef struct mochi_batch {
+  uint32_t n_grants;              /* N */
+  uint32_t n_certs;               /* C */
+  uint32_t n_ops;                 /* O = total transaction operations over all certificates */
+  uint32_t _pad0;
+  uint64_t grant_bytes_len;       /* size of grant_bytes                                      */
+  const uint8_t* grant_bytes;     /* blob holding every grant's proto3 bytes                  */
+  const uint64_t* grant_off;      /* [N] byte offset of grant i in grant_bytes                */
+  const uint32_t* grant_len;      /* [N] byte length of grant i (<= 65536)                    */
+  const uint8_t* sig;             /* [N * 256] big-endian RSA signatures                      */
+  const uint16_t* signer;         /* [N] key-table index of the signing server (MultiGrant.serverId) */
+  const uint8_t* grant_key;       /* [N] key slot of the op key this grant is for (< ops in cert) */
+  const uint32_t* cert_grant_off; /* [C+1] CSR: grants of cert c are [off[c], off[c+1])        */
+  const uint32_t* cert_op_off;    /* [C+1] CSR: ops of cert c are [off[c], off[c+1])           */
+  const uint8_t* op_key;          /* [O] key slot of each op (ops on the same key share a slot) */
+  const uint8_t* op_flags;        /* [O] MOCHI_OP_* bits                                        */
+  const uint8_t* expected_hash;   /* [C * 128] objectSHA512(txn) as lowercase hex (host-computed, §7.1.4) */
+} mochi_batch;
+
+typedef struct mochi_params {
+  uint32_t replication_factor; /* R = _CONFIG_BFT_REPLICATION; majority M = 2*(R/3)+1 */
+  uint32_t strict_gt;          /* 1: server predicate count > M (InMemoryDataStore.java:590)
+                                  0: client predicate count >= M (MochiDBClient.java:172,379) */
+  uint32_t _pad[2];
+} mochi_params;
+
+typedef struct mochi_verdicts {
+  uint32_t* grant_valid_bits; /* [ceil(N/32)] bit i = grant i signature valid  (may be NULL) */
+  uint8_t* grant_flags;       /* [N] MOCHI_GRANT_* bits                          (may be NULL) */
+  int64_t* grant_ts;          /* [N] parsed Grant.timestamp                      (may be NULL) */
+  uint32_t* cert_accept_bits; /* [ceil(C/32)] bit c = certificate accepted       (required)    */
+  uint8_t* cert_reason;       /* [C] enum mochi_reason                           (may be NULL) */
+  uint8_t* cert_fail_op;      /* [C] op index of the first failing op, 0xFF if none / n.a. (may be NULL) */
+} mochi_verdicts;
+
+typedef struct mochi_ctx mochi_ctx;
+
+/* ABI version of the loaded library (== MOCHI_ABI_VERSION). */
+int mochi_abi_version(void);
+
+/* Thread-local text of the last error returned on this thread. */
+const char* mochi_last_error(void);
+
+/* Number of visible HIP devices (0 when none). */
+int mochi_device_count(void);
+
+/*
+ * Create a verifier on HIP device `device` with a key table of `n_keys`
+ * RSA public keys.  `moduli_be` holds n_keys * key_bytes big-endian moduli
+ * (key_bytes must be 256; every modulus exactly 2048 bits and odd);
+ * `public_exponent` must be 65537.  Key index = MultiGrant.serverId's position
+ * in the table.  Montgomery constants (n0', R^2 mod n) are derived here and
+ * the table is uploaded once.  Returns NULL on error (see mochi_last_error()).
+ */
+mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_keys, uint32_t key_bytes,
+                            uint32_t public_exponent);
+void mochi_ctx_destroy(mochi_ctx* ctx);
+
+/*
+ * Verify a batch held in HOST memory: stages it through pinned buffers with
+ * hipMemcpyAsync on the context's stream, runs grant prep + RSA verify +
+ * certificate tally, copies the verdicts back.  Synchronous.  Thread-safe
+ * per context (calls on one context serialize).
+ */
+int mochi_verify_batch(mochi_ctx* ctx, const mochi_batch* batch, const mochi_params* params,
+                       mochi_verdicts* out);
+
+/*
+ * Verify a batch already resident in DEVICE memory (every mochi_batch pointer
+ * and every non-NULL mochi_verdicts pointer is a device pointer).  Enqueued on
+ * `stream` (a hipStream_t, NULL = the context's stream); asynchronous.  The
+ * batch header itself is read on the host.  Scratch is owned by the context.
+ */
+int mochi_verify_batch_device(mochi_ctx* ctx, const mochi_batch* batch, const mochi_params* params,
+                              mochi_verdicts* out, void* stream);
+
+/*
+ * The raw RSA public operation y = s^65537 mod n for n signatures (big-endian,
+ * 256 bytes each) under key `signer[i]`, on the device, through the same
+ * kernels as the verify path (k_rsa_pow + k_rsa_final).  out_be: n * 256
+ * bytes.  out_z (optional, n * 74 words): the squaring-chain intermediate
+ * z = s^(2^16) * R^-(2^16-1) mod n in radix-2^28 limbs (< 2n), for tests.
+ * Host memory, synchronous.
+ */
+int mochi_rsa_public_op(mochi_ctx* ctx, uint32_t n, const uint8_t* sig_be, const uint16_t* signer, uint8_t* out_be,
+                        uint32_t* out_z);
+
+/* Stream-event timings of the last mochi_verify_batch() call on this context:
+ * host->device copy, kernels, device->host copy (milliseconds). */
+int mochi_ctx_last_timing(mochi_ctx* ctx, float* h2d_ms, float* kernels_ms, float* d2h_ms);
+
+/*
+ * Producer side (the Write1 signing site the reference leaves as a TODO:
+ * InMemoryDataStore.java:283-295, MochiProtocol.proto:123): sign SHA-256 of
+ * each grant's bytes with an RSA-2048 private key (PEM, PKCS#1 v1.5,
+ * "SHA256withRSA"), CPU / OpenSSL, `n_threads` threads.  sig_out: n * 256.
+ */
+int mochi_sign_grants(const char* pem_private_key, uint32_t n, const uint8_t* grant_bytes, const uint64_t* grant_off,
+                      const uint32_t* grant_len, uint8_t* sig_out, int n_threads);
+
+/* Big-endian modulus of a PEM RSA key (private or public) -> n_be_out[256]. */
+int mochi_pem_modulus(const char* pem_key, uint8_t* n_be_out);
+
+/*
+ * Client-side response aggregation (MochiDBClient.java:148-175 reads,
+ * 355-382 Write2): for each request r, responses [resp_off[r], resp_off[r+1])
+ * each carry n_ops[r] op statuses (1 byte each, OperationResultStatus: 0 = OK,
+ * 1 = WRONG_SHARD) at status + status_off[resp]; resp_n_ops[resp] is the op
+ * count that response actually returned.  Request r is accepted iff every
+ * response returned n_ops[r] results and, for every op, the number of
+ * non-WRONG_SHARD results is >= M = 2*(R/3)+1.  chosen[status_off-aligned]
+ * receives, per (request, op), the index of the LAST non-WRONG_SHARD response
+ * (MochiDBClient.java:166,373) or -1.  reason[r]: 0 accept, 1 op-count
+ * mismatch (InconsistentRead/WriteException at :159-161 / :366-368), 2 below
+ * majority (:171-175 / :378-381).  Host memory; pure CPU.
+ */
+int mochi_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const uint32_t* n_ops,
+                          const uint32_t* resp_n_ops, const uint64_t* status_off, const uint8_t* status,
+                          const uint64_t* chosen_off, uint32_t replication_factor, int32_t* chosen,
+                          uint8_t* reason, uint32_t* accept_bits);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MOCHI_HIP_H */

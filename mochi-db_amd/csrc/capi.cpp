@@ -1,0 +1,556 @@
+// capi.cpp — libmochi_hip C ABI (include/mochi_hip.h): contexts, key tables,
+// device scratch, host<->device staging, and the client-side tally.
+//
+// The verify path it drives replaces, in the reference,
+//   InMemoryDataStore.processWrite2ToServer  (InMemoryDataStore.java:641-666)
+// with one batched call over many certificates.
+#include <hip/hip_runtime.h>
+#include <openssl/bn.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mochi_hip.h"
+#include "kernels.h"
+#include "mont.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) return fail(MOCHI_EHIP, "%s: %s", #expr, hipGetErrorString(e_));   \
+  } while (0)
+
+// Growable device allocation.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return MOCHI_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 256 ? 256 : bytes;
+    if (hipMalloc(&p, want) != hipSuccess) return fail(MOCHI_ENOMEM, "hipMalloc(%zu) failed", want);
+    cap = want;
+    return MOCHI_OK;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return MOCHI_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess)
+      return fail(MOCHI_ENOMEM, "hipHostMalloc(%zu) failed", want);
+    cap = want;
+    return MOCHI_OK;
+  }
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---- host-side key precompute (OpenSSL BN, setup only) --------------------
+int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
+  using namespace mochi;
+  memset(e, 0, sizeof *e);
+  if (!(n_be[0] & 0x80)) return fail(MOCHI_EINVAL, "modulus is not 2048 bits (top bit clear)");
+  if (!(n_be[255] & 1)) return fail(MOCHI_EINVAL, "modulus is even");
+  // 32-bit words, little-endian word order
+  for (int i = 0; i < 64; i++) {
+    const uint8_t* b = n_be + 256 - 4 * (i + 1);
+    e->n32[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+  }
+  auto to_limbs = [](const uint32_t* w, uint32_t* x) {
+    for (int j = 0; j < kL; j++) {
+      const int bit = j * kLimbBits, wi = bit >> 5, sh = bit & 31;
+      const uint64_t lo = wi < 64 ? w[wi] : 0, hi = wi + 1 < 64 ? w[wi + 1] : 0;
+      x[j] = (uint32_t)(((hi << 32) | lo) >> sh) & kLimbMask;
+    }
+  };
+  to_limbs(e->n32, e->n);
+  // n0inv = -n^{-1} mod 2^28 (Newton iteration on 32 bits)
+  uint32_t inv = 1;
+  for (int i = 0; i < 6; i++) inv *= 2u - e->n32[0] * inv;
+  e->n0inv = (0u - inv) & kLimbMask;
+  // kfix = R^65537 mod n, R = 2^(28*74)
+  BN_CTX* ctx = BN_CTX_new();
+  BIGNUM *n = BN_bin2bn(n_be, 256, nullptr), *r = BN_new(), *k = BN_new(), *ex = BN_new();
+  int ok = ctx && n && r && k && ex;
+  ok = ok && BN_set_bit(r, kL * kLimbBits) && BN_mod(r, r, n, ctx);
+  ok = ok && BN_set_word(ex, MOCHI_RSA_E) && BN_mod_exp(k, r, ex, n, ctx);
+  uint8_t kbe[256];
+  ok = ok && BN_bn2binpad(k, kbe, 256) == 256;
+  BN_free(n);
+  BN_free(r);
+  BN_free(k);
+  BN_free(ex);
+  BN_CTX_free(ctx);
+  if (!ok) return fail(MOCHI_EINVAL, "key precompute failed");
+  uint32_t kw[64];
+  for (int i = 0; i < 64; i++) {
+    const uint8_t* b = kbe + 256 - 4 * (i + 1);
+    kw[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+  }
+  to_limbs(kw, e->kfix);
+  return MOCHI_OK;
+}
+
+}  // namespace
+
+struct mochi_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t n_keys = 0;
+  mochi::KeyEntry* d_keys = nullptr;
+  std::mutex mu;
+  // verify scratch
+  DevBuf digest, ts, hash_off, hash_len, flags, count, cursor, total, perm, xbuf;
+  // host-path device copies
+  DevBuf dev_in, dev_out;
+  PinnedBuf pin_in, pin_out;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  float last_ms[3] = {0, 0, 0};  // h2d, kernels, d2h of the last host-path call
+};
+
+extern "C" {
+
+int mochi_abi_version(void) { return MOCHI_ABI_VERSION; }
+
+const char* mochi_last_error(void) { return g_err.c_str(); }
+
+int mochi_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_keys, uint32_t key_bytes,
+                            uint32_t public_exponent) {
+  if (!moduli_be || n_keys == 0 || n_keys > MOCHI_MAX_KEYS) {
+    fail(MOCHI_EINVAL, "n_keys must be in [1, %d]", MOCHI_MAX_KEYS);
+    return nullptr;
+  }
+  if (key_bytes != MOCHI_RSA_BYTES) {
+    fail(MOCHI_EINVAL, "key_bytes must be %d (RSA-2048)", MOCHI_RSA_BYTES);
+    return nullptr;
+  }
+  if (public_exponent != MOCHI_RSA_E) {
+    fail(MOCHI_EINVAL, "public_exponent must be 65537");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    fail(MOCHI_ENODEV, "no HIP device visible");
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev) {
+    fail(MOCHI_ENODEV, "device %d out of range (%d visible)", device, ndev);
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    fail(MOCHI_ENODEV, "device %d is not gfx950 (%s)", device, prop.gcnArchName);
+    return nullptr;
+  }
+  std::vector<mochi::KeyEntry> table(n_keys);
+  for (uint32_t k = 0; k < n_keys; k++)
+    if (make_key_entry(moduli_be + (size_t)k * MOCHI_RSA_BYTES, &table[k]) != MOCHI_OK) return nullptr;
+  mochi_ctx* c = new mochi_ctx;
+  c->device = device;
+  c->n_keys = n_keys;
+  int save = 0;
+  (void)hipGetDevice(&save);
+  bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc(&c->d_keys, sizeof(mochi::KeyEntry) * n_keys) == hipSuccess &&
+            hipMemcpy(c->d_keys, table.data(), sizeof(mochi::KeyEntry) * n_keys, hipMemcpyHostToDevice) == hipSuccess;
+  for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  (void)hipSetDevice(save);
+  if (!ok) {
+    fail(MOCHI_EHIP, "context setup failed on device %d", device);
+    mochi_ctx_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+void mochi_ctx_destroy(mochi_ctx* c) {
+  if (!c) return;
+  int save = 0;
+  (void)hipGetDevice(&save);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->d_keys) (void)hipFree(c->d_keys);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  (void)hipSetDevice(save);
+}
+
+}  // extern "C"
+
+namespace {
+
+int check_batch_header(const mochi_ctx* c, const mochi_batch* b, const mochi_params* p, const mochi_verdicts* o) {
+  if (!c || !b || !p || !o) return fail(MOCHI_EINVAL, "null argument");
+  if (!o->cert_accept_bits && b->n_certs) return fail(MOCHI_EINVAL, "cert_accept_bits is required");
+  if (p->replication_factor == 0) return fail(MOCHI_EINVAL, "replication_factor must be > 0");
+  if (b->n_grants && (!b->grant_bytes || !b->grant_off || !b->grant_len || !b->sig || !b->signer || !b->grant_key))
+    return fail(MOCHI_EINVAL, "grant arrays must be non-null when n_grants > 0");
+  if (!b->cert_grant_off || !b->cert_op_off) return fail(MOCHI_EINVAL, "cert_grant_off / cert_op_off required");
+  if (b->n_certs && !b->expected_hash) return fail(MOCHI_EINVAL, "expected_hash required");
+  if (b->n_ops && (!b->op_key || !b->op_flags)) return fail(MOCHI_EINVAL, "op arrays required");
+  return MOCHI_OK;
+}
+
+// Host-side consistency checks (host path only; the device path trusts the caller's device arrays).
+int check_batch_host(const mochi_batch* b) {
+  if (b->cert_grant_off[0] != 0 || b->cert_grant_off[b->n_certs] != b->n_grants)
+    return fail(MOCHI_EINVAL, "cert_grant_off must start at 0 and end at n_grants");
+  if (b->cert_op_off[0] != 0 || b->cert_op_off[b->n_certs] != b->n_ops)
+    return fail(MOCHI_EINVAL, "cert_op_off must start at 0 and end at n_ops");
+  for (uint32_t c = 0; c < b->n_certs; c++) {
+    if (b->cert_grant_off[c + 1] < b->cert_grant_off[c] || b->cert_op_off[c + 1] < b->cert_op_off[c])
+      return fail(MOCHI_EINVAL, "CSR offsets must be non-decreasing (cert %u)", c);
+    if (b->cert_op_off[c + 1] - b->cert_op_off[c] > MOCHI_MAX_OPS_PER_CERT)
+      return fail(MOCHI_EINVAL, "cert %u has more than %d ops", c, MOCHI_MAX_OPS_PER_CERT);
+  }
+  for (uint32_t i = 0; i < b->n_grants; i++) {
+    if (b->grant_len[i] > 65536) return fail(MOCHI_EINVAL, "grant %u longer than 65536 bytes", i);
+    if (b->grant_off[i] > b->grant_bytes_len || b->grant_len[i] > b->grant_bytes_len - b->grant_off[i])
+      return fail(MOCHI_EINVAL, "grant %u lies outside grant_bytes", i);
+  }
+  for (uint32_t o = 0; o < b->n_ops; o++)
+    if (b->op_key[o] >= MOCHI_MAX_OPS_PER_CERT) return fail(MOCHI_EINVAL, "op_key[%u] >= %d", o, MOCHI_MAX_OPS_PER_CERT);
+  return MOCHI_OK;
+}
+
+int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o, hipStream_t st) {
+  const uint32_t N = b->n_grants, C = b->n_certs;
+  const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
+  if (slots > 0xFFFFFFF0ull) return fail(MOCHI_EINVAL, "batch too large");
+  int rc;
+  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) ||
+      (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
+      (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
+      (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
+      (rc = c->total.ensure(sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
+      (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots)))
+    return rc;
+  mochi::LaunchArgs a;
+  memset(&a, 0, sizeof a);
+  a.n_grants = N;
+  a.n_certs = C;
+  a.n_keys = c->n_keys;
+  a.n_slots = (uint32_t)slots;
+  a.blob = b->grant_bytes;
+  a.grant_off = b->grant_off;
+  a.grant_len = b->grant_len;
+  a.sig = b->sig;
+  a.signer = b->signer;
+  a.grant_key = b->grant_key;
+  a.cert_grant_off = b->cert_grant_off;
+  a.cert_op_off = b->cert_op_off;
+  a.op_key = b->op_key;
+  a.op_flags = b->op_flags;
+  a.expected_hash = b->expected_hash;
+  const uint32_t R = p->replication_factor;
+  a.majority = 2 * (R / 3) + 1;  // ClusterConfiguration.getServerMajority  ClusterConfiguration.java:264-267
+  a.strict_gt = p->strict_gt ? 1 : 0;
+  a.keys = c->d_keys;
+  a.digest = c->digest.as<uint32_t>();
+  a.ts = o->grant_ts ? o->grant_ts : c->ts.as<int64_t>();
+  a.hash_off = c->hash_off.as<uint64_t>();
+  a.hash_len = c->hash_len.as<uint32_t>();
+  a.flags = o->grant_flags ? o->grant_flags : c->flags.as<uint8_t>();
+  a.count = c->count.as<uint32_t>();
+  a.cursor = c->cursor.as<uint32_t>();
+  a.total = c->total.as<uint32_t>();
+  a.perm = c->perm.as<uint32_t>();
+  a.xbuf = c->xbuf.as<uint32_t>();
+  a.grant_valid_bits = o->grant_valid_bits;
+  a.cert_accept_bits = o->cert_accept_bits;
+  a.cert_reason = o->cert_reason;
+  a.cert_fail_op = o->cert_fail_op;
+  HIP_TRY(mochi::launch_verify(a, st));
+  return MOCHI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mochi_verify_batch_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o,
+                              void* stream) {
+  int rc = check_batch_header(c, b, p, o);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  rc = run_device(c, b, p, o, stream ? (hipStream_t)stream : c->stream);
+  (void)hipSetDevice(save);
+  return rc;
+}
+
+int mochi_verify_batch(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o) {
+  int rc = check_batch_header(c, b, p, o);
+  if (rc) return rc;
+  if ((rc = check_batch_host(b))) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  const uint32_t N = b->n_grants, C = b->n_certs, O = b->n_ops;
+  // --- stage inputs: one pinned region, one H2D copy ---
+  struct Seg {
+    const void* src;
+    size_t bytes;
+    size_t off;
+  };
+  Seg in[] = {
+      {b->grant_bytes, (size_t)b->grant_bytes_len, 0},
+      {b->grant_off, sizeof(uint64_t) * N, 0},
+      {b->grant_len, sizeof(uint32_t) * N, 0},
+      {b->sig, (size_t)MOCHI_RSA_BYTES * N, 0},
+      {b->signer, sizeof(uint16_t) * N, 0},
+      {b->grant_key, (size_t)N, 0},
+      {b->cert_grant_off, sizeof(uint32_t) * (C + 1), 0},
+      {b->cert_op_off, sizeof(uint32_t) * (C + 1), 0},
+      {b->op_key, (size_t)O, 0},
+      {b->op_flags, (size_t)O, 0},
+      {b->expected_hash, (size_t)MOCHI_TXN_HASH_BYTES * C, 0},
+  };
+  size_t in_total = 0;
+  for (auto& s : in) {
+    s.off = in_total;
+    in_total = align_up(in_total + s.bytes, 256);
+  }
+  const size_t nbits_g = ((size_t)N + 31) / 32 * 4, nbits_c = ((size_t)C + 31) / 32 * 4;
+  Seg outs[] = {{o->grant_valid_bits, o->grant_valid_bits ? nbits_g : 0, 0},
+                {o->grant_flags, o->grant_flags ? (size_t)N : 0, 0},
+                {o->grant_ts, o->grant_ts ? sizeof(int64_t) * N : 0, 0},
+                {o->cert_accept_bits, nbits_c, 0},
+                {o->cert_reason, o->cert_reason ? (size_t)C : 0, 0},
+                {o->cert_fail_op, o->cert_fail_op ? (size_t)C : 0, 0}};
+  size_t out_total = 0;
+  for (auto& s : outs) {
+    s.off = out_total;
+    out_total = align_up(out_total + s.bytes, 256);
+  }
+  if ((rc = c->pin_in.ensure(in_total)) || (rc = c->dev_in.ensure(in_total)) || (rc = c->pin_out.ensure(out_total)) ||
+      (rc = c->dev_out.ensure(out_total))) {
+    (void)hipSetDevice(save);
+    return rc;
+  }
+  uint8_t* pin = (uint8_t*)c->pin_in.p;
+  for (auto& s : in)
+    if (s.bytes) memcpy(pin + s.off, s.src, s.bytes);
+  uint8_t* din = c->dev_in.as<uint8_t>();
+  uint8_t* dout = c->dev_out.as<uint8_t>();
+  hipStream_t st = c->stream;
+  (void)hipEventRecord(c->ev[0], st);
+  if (hipMemcpyAsync(din, pin, in_total, hipMemcpyHostToDevice, st) != hipSuccess) {
+    (void)hipSetDevice(save);
+    return fail(MOCHI_EHIP, "H2D copy failed");
+  }
+  (void)hipEventRecord(c->ev[1], st);
+  mochi_batch db = *b;
+  db.grant_bytes = din + in[0].off;
+  db.grant_off = (const uint64_t*)(din + in[1].off);
+  db.grant_len = (const uint32_t*)(din + in[2].off);
+  db.sig = din + in[3].off;
+  db.signer = (const uint16_t*)(din + in[4].off);
+  db.grant_key = din + in[5].off;
+  db.cert_grant_off = (const uint32_t*)(din + in[6].off);
+  db.cert_op_off = (const uint32_t*)(din + in[7].off);
+  db.op_key = din + in[8].off;
+  db.op_flags = din + in[9].off;
+  db.expected_hash = din + in[10].off;
+  mochi_verdicts dv;
+  dv.grant_valid_bits = o->grant_valid_bits ? (uint32_t*)(dout + outs[0].off) : nullptr;
+  dv.grant_flags = o->grant_flags ? dout + outs[1].off : nullptr;
+  dv.grant_ts = o->grant_ts ? (int64_t*)(dout + outs[2].off) : nullptr;
+  dv.cert_accept_bits = (uint32_t*)(dout + outs[3].off);
+  dv.cert_reason = o->cert_reason ? dout + outs[4].off : nullptr;
+  dv.cert_fail_op = o->cert_fail_op ? dout + outs[5].off : nullptr;
+  rc = run_device(c, &db, p, &dv, st);
+  if (rc) {
+    (void)hipSetDevice(save);
+    return rc;
+  }
+  (void)hipEventRecord(c->ev[2], st);
+  if (hipMemcpyAsync(c->pin_out.p, dout, out_total, hipMemcpyDeviceToHost, st) != hipSuccess) {
+    (void)hipSetDevice(save);
+    return fail(MOCHI_EHIP, "D2H copy failed");
+  }
+  (void)hipEventRecord(c->ev[3], st);
+  if (hipStreamSynchronize(st) != hipSuccess) {
+    (void)hipSetDevice(save);
+    return fail(MOCHI_EHIP, "stream sync failed: %s", hipGetErrorString(hipGetLastError()));
+  }
+  (void)hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[1]);
+  (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);
+  const uint8_t* pout = (const uint8_t*)c->pin_out.p;
+  void* dsts[] = {o->grant_valid_bits, o->grant_flags, o->grant_ts, o->cert_accept_bits, o->cert_reason,
+                  o->cert_fail_op};
+  for (int i = 0; i < 6; i++)
+    if (outs[i].bytes) memcpy(dsts[i], pout + outs[i].off, outs[i].bytes);
+  (void)hipSetDevice(save);
+  return MOCHI_OK;
+}
+
+int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const uint16_t* signer, uint8_t* out_be,
+                        uint32_t* out_z) {
+  if (!c || (n && (!sig_be || !signer || !out_be))) return fail(MOCHI_EINVAL, "null argument");
+  for (uint32_t i = 0; i < n; i++)
+    if (signer[i] >= c->n_keys) return fail(MOCHI_EINVAL, "signer[%u] out of range", i);
+  if (n == 0) return MOCHI_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  const uint64_t slots = mochi::slot_capacity(n, c->n_keys);
+  const size_t sig_bytes = (size_t)MOCHI_RSA_BYTES * n, y_bytes = sizeof(uint32_t) * 64 * (size_t)n;
+  int rc;
+  if ((rc = c->dev_in.ensure(align_up(sig_bytes, 256) + sizeof(uint16_t) * n)) || (rc = c->dev_out.ensure(y_bytes)) ||
+      (rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)n)) || (rc = c->flags.ensure(n)) ||
+      (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
+      (rc = c->total.ensure(sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
+      (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots))) {
+    (void)hipSetDevice(save);
+    return rc;
+  }
+  hipStream_t st = c->stream;
+  uint8_t* din = c->dev_in.as<uint8_t>();
+  uint16_t* dsigner = (uint16_t*)(din + align_up(sig_bytes, 256));
+  mochi::LaunchArgs a;
+  memset(&a, 0, sizeof a);
+  a.n_grants = n;
+  a.n_keys = c->n_keys;
+  a.n_slots = (uint32_t)slots;
+  a.sig = din;
+  a.signer = dsigner;
+  a.keys = c->d_keys;
+  a.digest = c->digest.as<uint32_t>();
+  a.flags = c->flags.as<uint8_t>();
+  a.count = c->count.as<uint32_t>();
+  a.cursor = c->cursor.as<uint32_t>();
+  a.total = c->total.as<uint32_t>();
+  a.perm = c->perm.as<uint32_t>();
+  a.xbuf = c->xbuf.as<uint32_t>();
+  a.dbg_y = c->dev_out.as<uint32_t>();
+  a.skip_prep_tally = true;
+  std::vector<uint32_t> y(64 * (size_t)n), perm, z;
+  bool ok = hipMemcpyAsync(din, sig_be, sig_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(dsigner, signer, sizeof(uint16_t) * n, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemsetAsync(a.digest, 0, sizeof(uint32_t) * 8 * (size_t)n, st) == hipSuccess &&
+            hipMemsetAsync(a.flags, 0, n, st) == hipSuccess && mochi::launch_verify(a, st) == hipSuccess &&
+            hipMemcpyAsync(y.data(), a.dbg_y, y_bytes, hipMemcpyDeviceToHost, st) == hipSuccess;
+  if (ok && out_z) {
+    perm.resize(slots);
+    z.resize((size_t)mochi::kL * slots);
+    ok = hipMemcpyAsync(perm.data(), a.perm, sizeof(uint32_t) * slots, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(z.data(), a.xbuf, sizeof(uint32_t) * z.size(), hipMemcpyDeviceToHost, st) == hipSuccess;
+  }
+  ok = ok && hipStreamSynchronize(st) == hipSuccess;
+  (void)hipSetDevice(save);
+  if (!ok) return fail(MOCHI_EHIP, "rsa_public_op failed: %s", hipGetErrorString(hipGetLastError()));
+  for (uint32_t g = 0; g < n; g++)
+    for (int i = 0; i < 64; i++) {
+      const uint32_t w = y[(size_t)g * 64 + i];
+      uint8_t* o = out_be + (size_t)g * 256 + 256 - 4 * (i + 1);
+      o[0] = (uint8_t)(w >> 24);
+      o[1] = (uint8_t)(w >> 16);
+      o[2] = (uint8_t)(w >> 8);
+      o[3] = (uint8_t)w;
+    }
+  if (out_z)
+    for (uint64_t sl = 0; sl < slots; sl++) {
+      const uint32_t g = perm[sl];
+      if (g == 0xFFFFFFFFu) continue;
+      for (int j = 0; j < mochi::kL; j++) out_z[(size_t)g * mochi::kL + j] = z[(size_t)j * slots + sl];
+    }
+  return MOCHI_OK;
+}
+
+int mochi_ctx_last_timing(mochi_ctx* c, float* h2d_ms, float* kernels_ms, float* d2h_ms) {
+  if (!c) return fail(MOCHI_EINVAL, "null ctx");
+  if (h2d_ms) *h2d_ms = c->last_ms[0];
+  if (kernels_ms) *kernels_ms = c->last_ms[1];
+  if (d2h_ms) *d2h_ms = c->last_ms[2];
+  return MOCHI_OK;
+}
+
+// Client-side aggregation: MochiDBClient.java:148-175 (reads) / 355-382 (Write2).
+int mochi_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const uint32_t* n_ops,
+                          const uint32_t* resp_n_ops, const uint64_t* status_off, const uint8_t* status,
+                          const uint64_t* chosen_off, uint32_t replication_factor, int32_t* chosen, uint8_t* reason,
+                          uint32_t* accept_bits) {
+  if (!resp_off || !n_ops || !resp_n_ops || !status_off || !status || !chosen_off || !accept_bits)
+    return fail(MOCHI_EINVAL, "null argument");
+  const uint32_t M = 2 * (replication_factor / 3) + 1;  // getServerMajority
+  memset(accept_bits, 0, ((size_t)n_requests + 31) / 32 * 4);
+  std::vector<uint32_t> cnt;
+  for (uint32_t r = 0; r < n_requests; r++) {
+    const uint32_t k = n_ops[r];
+    cnt.assign(k, 0);
+    int32_t* ch = chosen ? chosen + chosen_off[r] : nullptr;
+    if (ch)
+      for (uint32_t j = 0; j < k; j++) ch[j] = -1;
+    uint8_t why = 0;
+    for (uint32_t q = resp_off[r]; q < resp_off[r + 1]; q++) {
+      if (resp_n_ops[q] != k) {  // operations.size() != transactionOps.size()
+        why = 1;
+        break;
+      }
+      const uint8_t* st = status + status_off[q];
+      for (uint32_t j = 0; j < k; j++)
+        if (st[j] != 1) {  // != WRONG_SHARD
+          cnt[j]++;
+          if (ch) ch[j] = (int32_t)(q - resp_off[r]);
+        }
+    }
+    for (uint32_t j = 0; j < k && !why; j++)
+      if (cnt[j] < M) why = 2;  // consistentTRCount[index] < getServerMajority()
+    if (reason) reason[r] = why;
+    if (!why) accept_bits[r >> 5] |= 1u << (r & 31);
+  }
+  return MOCHI_OK;
+}
+
+}  // extern "C"

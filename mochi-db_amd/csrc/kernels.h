@@ -1,0 +1,57 @@
+// kernels.h — launch interface between the C-ABI layer (capi.cpp) and the
+// HIP kernels (kernels.hip).  All pointers are device pointers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mochi {
+
+struct KeyEntry;
+
+struct LaunchArgs {
+  // batch
+  uint32_t n_grants, n_certs, n_keys, n_slots;
+  const uint8_t* blob;
+  const uint64_t* grant_off;
+  const uint32_t* grant_len;
+  const uint8_t* sig;
+  const uint16_t* signer;
+  const uint8_t* grant_key;
+  const uint32_t* cert_grant_off;
+  const uint32_t* cert_op_off;
+  const uint8_t* op_key;
+  const uint8_t* op_flags;
+  const uint8_t* expected_hash;
+  uint32_t majority, strict_gt;
+  const KeyEntry* keys;
+  // scratch (context-owned)
+  uint32_t* digest;    // [8][N]
+  int64_t* ts;         // [N]
+  uint64_t* hash_off;  // [N]
+  uint32_t* hash_len;  // [N]
+  uint8_t* flags;      // [N]  (may be the caller's grant_flags output)
+  uint32_t* count;     // [n_keys]
+  uint32_t* cursor;    // [n_keys]
+  uint32_t* total;     // [1]
+  uint32_t* perm;      // [n_slots]
+  uint32_t* xbuf;      // [kL][n_slots]
+  // outputs
+  uint32_t* grant_valid_bits;  // may be null
+  uint32_t* cert_accept_bits;
+  uint8_t* cert_reason;   // may be null
+  uint8_t* cert_fail_op;  // may be null
+  // mochi_rsa_public_op only: raw s^65537 mod n words [N][64] (else null)
+  uint32_t* dbg_y;
+  bool skip_prep_tally;
+};
+
+// Slots of the signer-bucketed RSA grid: every bucket is padded to 64.
+inline uint64_t slot_capacity(uint32_t n_grants, uint32_t n_keys) {
+  return (uint64_t)n_grants + 64ull * (n_keys < n_grants ? n_keys : n_grants);
+}
+
+hipError_t launch_verify(const LaunchArgs& a, hipStream_t stream);
+void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream);
+void launch_rsa_final(const LaunchArgs& a, hipStream_t stream);
+
+}  // namespace mochi

@@ -1,0 +1,459 @@
+"""ctypes binding for libmochi_hip (include/mochi_hip.h).
+
+The host-side mirror of the reference's Write2 verification interface for
+tests, the benchmark and Python callers.  The product path is the HIP
+library; this module never falls back to a CPU implementation: if the shared
+library is missing or no gfx950 device is visible, constructing a Verifier
+raises.
+
+Reference interface mirrored (tomisetsu/mochi-db):
+  DataStore.processWrite2ToServer(Write2ToServer) -> Object
+      server/datastrore/DataStore.java:12, InMemoryDataStore.java:641-666
+  MochiDBClient read / Write2 aggregation
+      client/MochiDBClient.java:148-175, 355-382
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmochi_hip.so")
+
+RSA_BYTES = 256
+RSA_E = 65537
+TXN_HASH_BYTES = 128
+MAX_OPS_PER_CERT = 64
+
+# status codes
+OK, EINVAL, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4
+
+# reason codes (enum mochi_reason)
+ACCEPT = 0
+REJECT_TS_MISMATCH = 1
+REJECT_NO_GRANT = 2
+REJECT_BELOW_QUORUM = 3
+REJECT_HASH_MISMATCH = 4
+REJECT_NO_SVOC = 5
+REJECT_MALFORMED = 6
+REASON_NAMES = {
+    ACCEPT: "ACCEPT",
+    REJECT_TS_MISMATCH: "TS_MISMATCH",
+    REJECT_NO_GRANT: "NO_GRANT",
+    REJECT_BELOW_QUORUM: "BELOW_QUORUM",
+    REJECT_HASH_MISMATCH: "HASH_MISMATCH",
+    REJECT_NO_SVOC: "NO_SVOC",
+    REJECT_MALFORMED: "MALFORMED",
+}
+
+OP_LOCAL = 0x01
+OP_HAS_SVOC = 0x02
+GRANT_SIG_OK = 0x01
+GRANT_PARSED = 0x02
+
+
+class MochiError(RuntimeError):
+    pass
+
+
+class Batch_C(ctypes.Structure):
+    _fields_ = [
+        ("n_grants", ctypes.c_uint32),
+        ("n_certs", ctypes.c_uint32),
+        ("n_ops", ctypes.c_uint32),
+        ("_pad0", ctypes.c_uint32),
+        ("grant_bytes_len", ctypes.c_uint64),
+        ("grant_bytes", ctypes.c_void_p),
+        ("grant_off", ctypes.c_void_p),
+        ("grant_len", ctypes.c_void_p),
+        ("sig", ctypes.c_void_p),
+        ("signer", ctypes.c_void_p),
+        ("grant_key", ctypes.c_void_p),
+        ("cert_grant_off", ctypes.c_void_p),
+        ("cert_op_off", ctypes.c_void_p),
+        ("op_key", ctypes.c_void_p),
+        ("op_flags", ctypes.c_void_p),
+        ("expected_hash", ctypes.c_void_p),
+    ]
+
+
+class Params_C(ctypes.Structure):
+    _fields_ = [
+        ("replication_factor", ctypes.c_uint32),
+        ("strict_gt", ctypes.c_uint32),
+        ("_pad", ctypes.c_uint32 * 2),
+    ]
+
+
+class Verdicts_C(ctypes.Structure):
+    _fields_ = [
+        ("grant_valid_bits", ctypes.c_void_p),
+        ("grant_flags", ctypes.c_void_p),
+        ("grant_ts", ctypes.c_void_p),
+        ("cert_accept_bits", ctypes.c_void_p),
+        ("cert_reason", ctypes.c_void_p),
+        ("cert_fail_op", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libmochi_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise MochiError(f"{path} not built: run `make -C mochi-db_amd` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32
+    lib.mochi_abi_version.restype = ctypes.c_int
+    lib.mochi_last_error.restype = ctypes.c_char_p
+    lib.mochi_device_count.restype = ctypes.c_int
+    lib.mochi_ctx_create.restype = vp
+    lib.mochi_ctx_create.argtypes = [ctypes.c_int, vp, u32, u32, u32]
+    lib.mochi_ctx_destroy.argtypes = [vp]
+    lib.mochi_verify_batch.argtypes = [vp, ctypes.POINTER(Batch_C), ctypes.POINTER(Params_C), ctypes.POINTER(Verdicts_C)]
+    lib.mochi_verify_batch_device.argtypes = [vp, ctypes.POINTER(Batch_C), ctypes.POINTER(Params_C),
+                                              ctypes.POINTER(Verdicts_C), vp]
+    lib.mochi_ctx_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                          ctypes.POINTER(ctypes.c_float)]
+    lib.mochi_sign_grants.argtypes = [ctypes.c_char_p, u32, vp, vp, vp, vp, ctypes.c_int]
+    lib.mochi_pem_modulus.argtypes = [ctypes.c_char_p, vp]
+    lib.mochi_rsa_public_op.argtypes = [vp, u32, vp, vp, vp, vp]
+    lib.mochi_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
+    if lib.mochi_abi_version() != 1:
+        raise MochiError("libmochi_hip ABI mismatch")
+    _lib = lib
+    return lib
+
+
+def _ptr(a: Optional[np.ndarray]) -> Optional[int]:
+    if a is None:
+        return None
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("arrays must be C-contiguous")
+    return a.ctypes.data
+
+
+def _err(lib) -> str:
+    return (lib.mochi_last_error() or b"").decode(errors="replace")
+
+
+@dataclass
+class Batch:
+    """A batch of Write2 certificates, struct-of-arrays (see mochi_batch)."""
+
+    grant_bytes: np.ndarray  # uint8 blob
+    grant_off: np.ndarray  # uint64 [N]
+    grant_len: np.ndarray  # uint32 [N]
+    sig: np.ndarray  # uint8 [N, 256]
+    signer: np.ndarray  # uint16 [N]
+    grant_key: np.ndarray  # uint8 [N]
+    cert_grant_off: np.ndarray  # uint32 [C+1]
+    cert_op_off: np.ndarray  # uint32 [C+1]
+    op_key: np.ndarray  # uint8 [O]
+    op_flags: np.ndarray  # uint8 [O]
+    expected_hash: np.ndarray  # uint8 [C, 128]
+
+    @property
+    def n_grants(self) -> int:
+        return int(self.grant_off.shape[0])
+
+    @property
+    def n_certs(self) -> int:
+        return int(self.cert_grant_off.shape[0]) - 1
+
+    @property
+    def n_ops(self) -> int:
+        return int(self.op_key.shape[0])
+
+    def normalized(self) -> "Batch":
+        return Batch(
+            grant_bytes=np.ascontiguousarray(self.grant_bytes, dtype=np.uint8),
+            grant_off=np.ascontiguousarray(self.grant_off, dtype=np.uint64),
+            grant_len=np.ascontiguousarray(self.grant_len, dtype=np.uint32),
+            sig=np.ascontiguousarray(self.sig, dtype=np.uint8).reshape(-1, RSA_BYTES),
+            signer=np.ascontiguousarray(self.signer, dtype=np.uint16),
+            grant_key=np.ascontiguousarray(self.grant_key, dtype=np.uint8),
+            cert_grant_off=np.ascontiguousarray(self.cert_grant_off, dtype=np.uint32),
+            cert_op_off=np.ascontiguousarray(self.cert_op_off, dtype=np.uint32),
+            op_key=np.ascontiguousarray(self.op_key, dtype=np.uint8),
+            op_flags=np.ascontiguousarray(self.op_flags, dtype=np.uint8),
+            expected_hash=np.ascontiguousarray(self.expected_hash, dtype=np.uint8).reshape(-1, TXN_HASH_BYTES),
+        )
+
+    def to_c(self) -> Batch_C:
+        b = Batch_C()
+        b.n_grants, b.n_certs, b.n_ops = self.n_grants, self.n_certs, self.n_ops
+        b.grant_bytes_len = int(self.grant_bytes.nbytes)
+        b.grant_bytes = _ptr(self.grant_bytes)
+        b.grant_off = _ptr(self.grant_off)
+        b.grant_len = _ptr(self.grant_len)
+        b.sig = _ptr(self.sig)
+        b.signer = _ptr(self.signer)
+        b.grant_key = _ptr(self.grant_key)
+        b.cert_grant_off = _ptr(self.cert_grant_off)
+        b.cert_op_off = _ptr(self.cert_op_off)
+        b.op_key = _ptr(self.op_key)
+        b.op_flags = _ptr(self.op_flags)
+        b.expected_hash = _ptr(self.expected_hash)
+        return b
+
+
+@dataclass
+class Verdicts:
+    grant_valid_bits: np.ndarray
+    grant_flags: np.ndarray
+    grant_ts: np.ndarray
+    cert_accept_bits: np.ndarray
+    cert_reason: np.ndarray
+    cert_fail_op: np.ndarray
+    timing_ms: dict = field(default_factory=dict)
+
+    @staticmethod
+    def alloc(n_grants: int, n_certs: int) -> "Verdicts":
+        return Verdicts(
+            grant_valid_bits=np.zeros((n_grants + 31) // 32, np.uint32),
+            grant_flags=np.zeros(n_grants, np.uint8),
+            grant_ts=np.zeros(n_grants, np.int64),
+            cert_accept_bits=np.zeros((n_certs + 31) // 32, np.uint32),
+            cert_reason=np.zeros(n_certs, np.uint8),
+            cert_fail_op=np.zeros(n_certs, np.uint8),
+        )
+
+    def to_c(self) -> Verdicts_C:
+        v = Verdicts_C()
+        v.grant_valid_bits = _ptr(self.grant_valid_bits)
+        v.grant_flags = _ptr(self.grant_flags)
+        v.grant_ts = _ptr(self.grant_ts)
+        v.cert_accept_bits = _ptr(self.cert_accept_bits)
+        v.cert_reason = _ptr(self.cert_reason)
+        v.cert_fail_op = _ptr(self.cert_fail_op)
+        return v
+
+    @property
+    def grant_valid(self) -> np.ndarray:
+        return unpack_bits(self.grant_valid_bits, self.grant_flags.shape[0])
+
+    @property
+    def cert_accept(self) -> np.ndarray:
+        return unpack_bits(self.cert_accept_bits, self.cert_reason.shape[0])
+
+
+def unpack_bits(words: np.ndarray, n: int) -> np.ndarray:
+    """uint32 little-endian bitmap -> bool[n] (bit i of word i//32)."""
+    b = np.unpackbits(np.ascontiguousarray(words, dtype="<u4").view(np.uint8), bitorder="little")
+    return b[:n].astype(bool)
+
+
+def majority(replication_factor: int) -> int:
+    """ClusterConfiguration.getServerMajority (ClusterConfiguration.java:264-267)."""
+    return 2 * (replication_factor // 3) + 1
+
+
+class Verifier:
+    """A libmochi_hip context: one device, one RSA public-key table.
+
+    Key index i corresponds to the i-th server ID of the cluster (the
+    MultiGrant.serverId that signed the grant).
+    """
+
+    def __init__(self, moduli_be: Sequence[bytes] | np.ndarray, device: int = 0):
+        self.lib = load_library()
+        mod = np.ascontiguousarray(
+            np.frombuffer(b"".join(bytes(m) for m in moduli_be), np.uint8)
+            if not isinstance(moduli_be, np.ndarray) else moduli_be.astype(np.uint8).reshape(-1)
+        )
+        if mod.size % RSA_BYTES:
+            raise ValueError("moduli must be 256-byte big-endian values")
+        self.n_keys = mod.size // RSA_BYTES
+        self._moduli = mod
+        self.ctx = self.lib.mochi_ctx_create(int(device), mod.ctypes.data, self.n_keys, RSA_BYTES, RSA_E)
+        if not self.ctx:
+            raise MochiError(f"mochi_ctx_create failed: {_err(self.lib)}")
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.mochi_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def verify(self, batch: Batch, replication_factor: int, strict_gt: bool = True) -> Verdicts:
+        """Host-memory batch -> verdicts (pinned staging, synchronous)."""
+        b = batch.normalized()
+        out = Verdicts.alloc(b.n_grants, b.n_certs)
+        bc, vc = b.to_c(), out.to_c()
+        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        rc = self.lib.mochi_verify_batch(self.ctx, ctypes.byref(bc), ctypes.byref(p), ctypes.byref(vc))
+        if rc != OK:
+            raise MochiError(f"mochi_verify_batch rc={rc}: {_err(self.lib)}")
+        h, k, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        self.lib.mochi_ctx_last_timing(self.ctx, ctypes.byref(h), ctypes.byref(k), ctypes.byref(d))
+        out.timing_ms = {"h2d": h.value, "kernels": k.value, "d2h": d.value}
+        return out
+
+    def verify_device(self, dev: "DeviceBatch", out: "DeviceVerdicts", replication_factor: int,
+                      strict_gt: bool = True, stream: int = 0) -> None:
+        """Device-resident batch (torch tensors) -> device verdicts; async on `stream`."""
+        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        bc, vc = dev.to_c(), out.to_c()
+        rc = self.lib.mochi_verify_batch_device(self.ctx, ctypes.byref(bc), ctypes.byref(p), ctypes.byref(vc),
+                                                stream or None)
+        if rc != OK:
+            raise MochiError(f"mochi_verify_batch_device rc={rc}: {_err(self.lib)}")
+
+
+def rsa_public_op(verifier: "Verifier", sigs: np.ndarray, signer: np.ndarray, want_z: bool = False):
+    """y = s^65537 mod n on the device (big-endian bytes); optionally the chain intermediate z."""
+    lib = verifier.lib
+    s = np.ascontiguousarray(sigs, np.uint8).reshape(-1, RSA_BYTES)
+    sg = np.ascontiguousarray(signer, np.uint16)
+    n = s.shape[0]
+    out = np.zeros((n, RSA_BYTES), np.uint8)
+    z = np.zeros((n, 74), np.uint32) if want_z else None
+    rc = lib.mochi_rsa_public_op(verifier.ctx, n, _ptr(s), _ptr(sg), _ptr(out), _ptr(z) if want_z else None)
+    if rc != OK:
+        raise MochiError(f"mochi_rsa_public_op rc={rc}: {_err(lib)}")
+    return (out, z) if want_z else out
+
+
+class DeviceBatch:
+    """A Batch copied into device memory with torch (plumbing only)."""
+
+    def __init__(self, batch: Batch, device: int = 0):
+        import torch
+
+        b = batch.normalized()
+        dev = torch.device("cuda", device)
+
+        def t(a):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+        self.n_grants, self.n_certs, self.n_ops = b.n_grants, b.n_certs, b.n_ops
+        self.grant_bytes = t(b.grant_bytes)
+        self.grant_off = t(b.grant_off.view(np.int64))
+        self.grant_len = t(b.grant_len.view(np.int32))
+        self.sig = t(b.sig)
+        self.signer = t(b.signer.view(np.int16))
+        self.grant_key = t(b.grant_key)
+        self.cert_grant_off = t(b.cert_grant_off.view(np.int32))
+        self.cert_op_off = t(b.cert_op_off.view(np.int32))
+        self.op_key = t(b.op_key)
+        self.op_flags = t(b.op_flags)
+        self.expected_hash = t(b.expected_hash)
+
+    def to_c(self) -> Batch_C:
+        b = Batch_C()
+        b.n_grants, b.n_certs, b.n_ops = self.n_grants, self.n_certs, self.n_ops
+        b.grant_bytes_len = int(self.grant_bytes.numel())
+        for name in ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off",
+                     "cert_op_off", "op_key", "op_flags", "expected_hash"):
+            setattr(b, name, getattr(self, name).data_ptr())
+        return b
+
+
+class DeviceVerdicts:
+    def __init__(self, n_grants: int, n_certs: int, device: int = 0, full: bool = True):
+        import torch
+
+        dev = torch.device("cuda", device)
+        self.n_grants, self.n_certs = n_grants, n_certs
+        self.cert_accept_bits = torch.zeros((n_certs + 31) // 32, dtype=torch.int32, device=dev)
+        self.grant_valid_bits = torch.zeros((n_grants + 31) // 32, dtype=torch.int32, device=dev)
+        self.grant_flags = torch.zeros(n_grants, dtype=torch.uint8, device=dev) if full else None
+        self.grant_ts = torch.zeros(n_grants, dtype=torch.int64, device=dev) if full else None
+        self.cert_reason = torch.zeros(n_certs, dtype=torch.uint8, device=dev) if full else None
+        self.cert_fail_op = torch.zeros(n_certs, dtype=torch.uint8, device=dev) if full else None
+
+    def to_c(self) -> Verdicts_C:
+        v = Verdicts_C()
+        for name in ("grant_valid_bits", "grant_flags", "grant_ts", "cert_accept_bits", "cert_reason", "cert_fail_op"):
+            t = getattr(self, name)
+            setattr(v, name, t.data_ptr() if t is not None else None)
+        return v
+
+    def to_host(self) -> Verdicts:
+        def h(t, dt):
+            return t.cpu().numpy().view(dt) if t is not None else None
+
+        return Verdicts(
+            grant_valid_bits=h(self.grant_valid_bits, np.uint32),
+            grant_flags=h(self.grant_flags, np.uint8),
+            grant_ts=h(self.grant_ts, np.int64),
+            cert_accept_bits=h(self.cert_accept_bits, np.uint32),
+            cert_reason=h(self.cert_reason, np.uint8),
+            cert_fail_op=h(self.cert_fail_op, np.uint8),
+        )
+
+
+def sign_grants(pem_private_key: bytes, grant_bytes: np.ndarray, grant_off: np.ndarray, grant_len: np.ndarray,
+                n_threads: int = 8) -> np.ndarray:
+    """Producer-side SHA256withRSA signing of grants (libmochi_hip, OpenSSL)."""
+    lib = load_library()
+    blob = np.ascontiguousarray(grant_bytes, np.uint8)
+    off = np.ascontiguousarray(grant_off, np.uint64)
+    ln = np.ascontiguousarray(grant_len, np.uint32)
+    n = off.shape[0]
+    out = np.zeros((n, RSA_BYTES), np.uint8)
+    rc = lib.mochi_sign_grants(pem_private_key, n, _ptr(blob), _ptr(off), _ptr(ln), _ptr(out), int(n_threads))
+    if rc != OK:
+        raise MochiError(f"mochi_sign_grants rc={rc}")
+    return out
+
+
+def pem_modulus(pem: bytes) -> bytes:
+    lib = load_library()
+    out = np.zeros(RSA_BYTES, np.uint8)
+    if lib.mochi_pem_modulus(pem, _ptr(out)) != OK:
+        raise MochiError("not an RSA-2048 PEM key")
+    return out.tobytes()
+
+
+def tally_responses(responses: Sequence[Sequence[Sequence[int]]], n_ops: Sequence[int], replication_factor: int):
+    """Client aggregation (MochiDBClient.java:148-175 / 355-382) via libmochi_hip.
+
+    responses[r] = list of per-response status lists.  Returns (accept[bool],
+    reason[uint8], chosen[list of int arrays]).
+    """
+    lib = load_library()
+    nreq = len(responses)
+    resp_off = np.zeros(nreq + 1, np.uint32)
+    resp_n_ops, status_off, status, chosen_off = [], [], [], np.zeros(nreq, np.uint64)
+    pos = 0
+    cpos = 0
+    for r, resps in enumerate(responses):
+        resp_off[r + 1] = resp_off[r] + len(resps)
+        chosen_off[r] = cpos
+        cpos += n_ops[r]
+        for st in resps:
+            resp_n_ops.append(len(st))
+            status_off.append(pos)
+            status.extend(st)
+            pos += len(st)
+    n_ops_a = np.asarray(n_ops, np.uint32)
+    resp_n_ops_a = np.asarray(resp_n_ops if resp_n_ops else [0], np.uint32)
+    status_off_a = np.asarray(status_off if status_off else [0], np.uint64)
+    status_a = np.asarray(status if status else [0], np.uint8)
+    chosen = np.full(max(cpos, 1), -1, np.int32)
+    reason = np.zeros(max(nreq, 1), np.uint8)
+    bits = np.zeros(max((nreq + 31) // 32, 1), np.uint32)
+    rc = lib.mochi_tally_responses(nreq, _ptr(resp_off), _ptr(n_ops_a), _ptr(resp_n_ops_a), _ptr(status_off_a),
+                                   _ptr(status_a), _ptr(chosen_off), replication_factor, _ptr(chosen), _ptr(reason),
+                                   _ptr(bits))
+    if rc != OK:
+        raise MochiError(f"mochi_tally_responses rc={rc}: {_err(lib)}")
+    acc = unpack_bits(bits, nreq)
+    ch = [chosen[int(chosen_off[r]):int(chosen_off[r]) + n_ops[r]].copy() for r in range(nreq)]
+    return acc, reason[:nreq].copy(), ch

@@ -1,0 +1,256 @@
+"""Synthetic signed-grant workload.
+
+Certificates look like the ones MochiDB's Write2 path receives
+(InMemoryDataStore.java:641-666): R MultiGrants (one per replica, wire order
+= server index), each holding one Grant per transaction op, every grant
+signed by its server (SHA256withRSA).  Because CPU RSA signing is slow, a pool
+of unique signed grant templates is signed once and batches are built by
+seeded sampling from it; any certificate index regenerates independently
+(splitmix64 of the seed and the index), so shards can be built per rank.
+
+Fault mix per certificate (seeded): 1% one flipped signature bit, 0.5% one
+replica with timestamp + 1 (validly signed), 0.5% a wrong transactionHash on
+g0, 0.5% one replica missing, 0.25% a wrong hash on g1 (must still accept:
+the reference checks only g0, InMemoryDataStore.java:588-591).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from mochi_hip import (OP_HAS_SVOC, OP_LOCAL, RSA_BYTES, TXN_HASH_BYTES, Batch, pem_modulus, sign_grants)
+
+SEED = 0x4D4F434849  # "MOCHI"
+
+# Replica IDs of config/sample_config:1 in token order 0..3 (every key maps to
+# tokens 0..R-1 because of ClusterConfiguration.java:215), plus synthetic ones.
+SERVER_IDS = [
+    "server-ed25bc93-1047-4242-b87b-2246355b020b",
+    "server-55a78d3f-783d-43ae-95c1-6d0f5f02fe0c",
+    "server-6c023c90-87ed-40d9-8f38-48cb03fa2135",
+    "server-6a3b63b2-9fc8-4f3d-97c1-0f61cb244a0c",
+    "server-synthetic-r7-0004",
+    "server-synthetic-r7-0005",
+    "server-synthetic-r7-0006",
+]
+
+DEFAULT_KEY_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "keys")
+
+FAULT_NONE, FAULT_FLIP, FAULT_TS, FAULT_G0_HASH, FAULT_DROP, FAULT_G1_HASH = 0, 1, 2, 3, 4, 5
+# cumulative thresholds out of 10000
+_FAULT_TABLE = [(100, FAULT_FLIP), (150, FAULT_TS), (200, FAULT_G0_HASH), (250, FAULT_DROP), (275, FAULT_G1_HASH)]
+
+
+# ---------------------------------------------------------------------------
+# Grant encoding (producer side) — Grant.writeTo, MochiProtocol.java:7556-7574
+# ---------------------------------------------------------------------------
+def _varint(v: int) -> bytes:
+    v &= (1 << 64) - 1
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def encode_grant(object_id: str, timestamp: int, transaction_hash: str, configstamp: int = 0, status: int = 0) -> bytes:
+    out = bytearray()
+    oid = object_id.encode("utf-8")
+    th = transaction_hash.encode("utf-8")
+    if oid:
+        out += b"\x0a" + _varint(len(oid)) + oid
+    if timestamp:
+        out += b"\x10" + _varint(timestamp)
+    if configstamp:
+        out += b"\x18" + _varint(configstamp)
+    if th:
+        out += b"\x22" + _varint(len(th)) + th
+    if status:
+        out += b"\x28" + _varint(status)
+    return bytes(out)
+
+
+def txn_hash_hex(p: int) -> str:
+    """Stand-in for Utils.objectSHA512(txn) (Utils.java:150-153): lowercase hex SHA-512."""
+    return hashlib.sha512(f"txn-{p}".encode()).hexdigest()
+
+
+# ---------------------------------------------------------------------------
+# splitmix64 (vectorized)
+# ---------------------------------------------------------------------------
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = (np.asarray(x, dtype=np.uint64) + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _h(seed: int, stream: int, idx: np.ndarray) -> np.ndarray:
+    base = splitmix64(np.uint64((seed * 0x100000001B3 + stream) & 0xFFFFFFFFFFFFFFFF))
+    with np.errstate(over="ignore"):
+        return splitmix64(np.asarray(idx, np.uint64) ^ base)
+
+
+def load_keys(n: int, key_dir: str = DEFAULT_KEY_DIR) -> List[bytes]:
+    keys = []
+    for i in range(n):
+        with open(os.path.join(key_dir, f"server{i}.pem"), "rb") as f:
+            keys.append(f.read())
+    return keys
+
+
+@dataclass
+class Pool:
+    """Signed grant templates: normal[P, k, R] and fault variants[P_f, k, R]."""
+
+    R: int
+    k: int
+    P: int
+    P_f: int
+    blob: np.ndarray  # uint8
+    off: np.ndarray  # uint64 [3, P, k, R]  (variant 0 normal, 1 ts+1, 2 evil hash; variants valid for p < P_f)
+    length: np.ndarray  # uint32 [3, P, k, R]
+    sig: np.ndarray  # uint8 [3, P, k, R, 256]
+    expected_hash: np.ndarray  # uint8 [P, 128]
+    moduli: List[bytes]
+    key_pems: List[bytes]
+
+
+def _template_fields(p: int, j: int, k: int, seed: int):
+    oid = f"DEMO_KEY_STRESS_TEST_{(p * k + j) % 200}"
+    hp = int(_h(seed, 7, np.array([p]))[0])
+    ts = 1000 * ((p + j) % 64) + (hp % 1000)
+    return oid, ts
+
+
+def build_pool(R: int, k: int = 1, P: int = 4096, P_f: int = 256, seed: int = SEED, key_dir: str = DEFAULT_KEY_DIR,
+               n_threads: Optional[int] = None, cache_dir: Optional[str] = None) -> Pool:
+    if n_threads is None:
+        n_threads = min(16, os.cpu_count() or 1)
+    P_f = min(P_f, P)
+    pems = load_keys(R, key_dir)
+    cache = None
+    if cache_dir:
+        os.makedirs(cache_dir, exist_ok=True)
+        tag = hashlib.sha256(b"".join(pems) + f"{R}/{k}/{P}/{P_f}/{seed}/v1".encode()).hexdigest()[:16]
+        cache = os.path.join(cache_dir, f"pool_{tag}.npz")
+        if os.path.exists(cache):
+            z = np.load(cache)
+            return Pool(R, k, P, P_f, z["blob"], z["off"], z["length"], z["sig"], z["expected_hash"],
+                        [pem_modulus(p) for p in pems], pems)
+    chunks: List[bytes] = []
+    off = np.zeros((3, P, k, R), np.uint64)
+    length = np.zeros((3, P, k, R), np.uint32)
+    pos = 0
+    expected = np.zeros((P, TXN_HASH_BYTES), np.uint8)
+    for p in range(P):
+        th = txn_hash_hex(p)
+        expected[p] = np.frombuffer(th.encode(), np.uint8)
+        evil = hashlib.sha512(f"txn-{p}-evil".encode()).hexdigest()
+        for j in range(k):
+            oid, ts = _template_fields(p, j, k, seed)
+            variants = [encode_grant(oid, ts, th)]
+            if p < P_f:
+                variants += [encode_grant(oid, ts + 1, th), encode_grant(oid, ts, evil)]
+            for v, g in enumerate(variants):
+                # every replica signs the same grant bytes (one copy in the blob)
+                off[v, p, j, :] = pos
+                length[v, p, j, :] = len(g)
+                chunks.append(g)
+                pos += len(g)
+    blob = np.frombuffer(b"".join(chunks), np.uint8).copy()
+    sig = np.zeros((3, P, k, R, RSA_BYTES), np.uint8)
+    nv = np.array([3 if p < P_f else 1 for p in range(P)])
+    for r in range(R):
+        sel = [(v, p, j) for p in range(P) for j in range(k) for v in range(nv[p])]
+        vi = np.array([s[0] for s in sel]); pi = np.array([s[1] for s in sel]); ji = np.array([s[2] for s in sel])
+        s = sign_grants(pems[r], blob, off[vi, pi, ji, r], length[vi, pi, ji, r], n_threads)
+        sig[vi, pi, ji, r] = s
+    pool = Pool(R, k, P, P_f, blob, off, length, sig, expected, [pem_modulus(p) for p in pems], pems)
+    if cache:
+        np.savez(cache, blob=blob, off=off, length=length, sig=sig, expected_hash=expected)
+    return pool
+
+
+@dataclass
+class Synth:
+    batch: Batch
+    template: np.ndarray  # [C] pool template per certificate
+    fault: np.ndarray  # [C] FAULT_*
+    fault_replica: np.ndarray  # [C]
+    expected_flags: np.ndarray  # [N] uint8 ground-truth MOCHI_GRANT_* bits
+
+
+def make_batch(pool: Pool, n_certs: int, first_cert: int = 0, seed: int = SEED, faults: bool = True,
+               local_flags: int = OP_LOCAL | OP_HAS_SVOC) -> Synth:
+    """Certificates [first_cert, first_cert + n_certs) of the seeded stream."""
+    R, k, P, P_f = pool.R, pool.k, pool.P, pool.P_f
+    cidx = np.arange(first_cert, first_cert + n_certs, dtype=np.uint64)
+    p = (_h(seed, 1, cidx) % np.uint64(P)).astype(np.int64)
+    fault = np.zeros(n_certs, np.int64)
+    if faults:
+        u = (_h(seed, 2, cidx) % np.uint64(10000)).astype(np.int64)
+        lo = 0
+        for hi, f in _FAULT_TABLE:
+            fault[(u >= lo) & (u < hi)] = f
+            lo = hi
+    rf = (_h(seed, 3, cidx) % np.uint64(R)).astype(np.int64)
+    rf[fault == FAULT_G0_HASH] = 0
+    rf[fault == FAULT_G1_HASH] = 1 % R
+    p[fault != FAULT_NONE] %= P_f
+    # grid [C, R, k]
+    variant = np.zeros((n_certs, R, k), np.int64)
+    rr = np.arange(R)[None, :, None]
+    shape = (n_certs, R, k)
+    is_rf = np.broadcast_to(rr == rf[:, None, None], shape)
+    f3 = np.broadcast_to(fault[:, None, None], shape)
+    variant[(f3 == FAULT_TS) & is_rf] = 1
+    variant[((f3 == FAULT_G0_HASH) | (f3 == FAULT_G1_HASH)) & is_rf] = 2
+    keep = np.ones(shape, bool)
+    keep[(f3 == FAULT_DROP) & is_rf] = False
+    P3 = np.broadcast_to(p[:, None, None], keep.shape)
+    R3 = np.broadcast_to(rr, keep.shape)
+    J3 = np.broadcast_to(np.arange(k)[None, None, :], keep.shape)
+    sel = keep.reshape(-1)
+    vv, pp, r_, jj = variant.reshape(-1)[sel], P3.reshape(-1)[sel], R3.reshape(-1)[sel], J3.reshape(-1)[sel]
+    goff = pool.off[vv, pp, jj, r_]
+    glen = pool.length[vv, pp, jj, r_]
+    sig = pool.sig[vv, pp, jj, r_].copy()
+    n = goff.shape[0]
+    flags = np.full(n, 0x03, np.uint8)  # PARSED | SIG_OK
+    per_cert = keep.reshape(n_certs, -1).sum(1)
+    cert_grant_off = np.zeros(n_certs + 1, np.uint32)
+    np.cumsum(per_cert, out=cert_grant_off[1:])
+    # bit flip in replica rf's op-0 grant
+    flip_c = np.nonzero(fault == FAULT_FLIP)[0]
+    if flip_c.size:
+        # position of (c, rf, j=0) within the flattened kept grants (no drops in flip certs)
+        gi = cert_grant_off[flip_c].astype(np.int64) + rf[flip_c] * k
+        bit = (_h(seed, 4, cidx[flip_c]) % np.uint64(2048)).astype(np.int64)
+        sig[gi, bit // 8] ^= (1 << (bit % 8)).astype(np.uint8)
+        flags[gi] = 0x02
+    ops = np.tile(np.arange(k, dtype=np.uint8), n_certs)
+    batch = Batch(
+        grant_bytes=pool.blob,
+        grant_off=goff.astype(np.uint64),
+        grant_len=glen.astype(np.uint32),
+        sig=sig,
+        signer=r_.astype(np.uint16),
+        grant_key=jj.astype(np.uint8),
+        cert_grant_off=cert_grant_off,
+        cert_op_off=(np.arange(n_certs + 1, dtype=np.uint64) * k).astype(np.uint32),
+        op_key=ops,
+        op_flags=np.full(n_certs * k, local_flags, np.uint8),
+        expected_hash=pool.expected_hash[p],
+    )
+    return Synth(batch, p, fault, rf, flags)
+
+
+def n_certs_for_grants(n_grants: int, R: int, k: int = 1) -> int:
+    return max(1, n_grants // (R * k))

@@ -1,0 +1,277 @@
+"""HIP path vs the CPU oracle, bit-exact (needs an MI355X).
+
+Every test calls libmochi_hip through its C ABI (ctypes) and compares grant
+flags / timestamps / validity bits and certificate accept bits / reason codes /
+failing-op indices with oracle/ (OpenSSL + the restated Java verdict logic).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import mochi_hip as mh
+import oracle_ffi as O
+import workload as W
+from cases import build_case_batch, grouped_cases, moduli_for
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def pool4():
+    return W.build_pool(R=4, k=1, P=1024, P_f=128)
+
+
+@pytest.fixture(scope="module")
+def pool4k2():
+    return W.build_pool(R=4, k=2, P=512, P_f=64)
+
+
+@pytest.fixture(scope="module")
+def pool7():
+    return W.build_pool(R=7, k=1, P=1024, P_f=128)
+
+
+@pytest.fixture(scope="module")
+def ver4(pool4):
+    v = mh.Verifier(pool4.moduli, 0)
+    yield v
+    v.close()
+
+
+@pytest.fixture(scope="module")
+def ver7(pool7):
+    v = mh.Verifier(pool7.moduli, 0)
+    yield v
+    v.close()
+
+
+def assert_same(g: mh.Verdicts, o: mh.Verdicts, what=""):
+    np.testing.assert_array_equal(g.grant_flags, o.grant_flags, err_msg=f"grant_flags {what}")
+    np.testing.assert_array_equal(g.grant_ts, o.grant_ts, err_msg=f"grant_ts {what}")
+    np.testing.assert_array_equal(g.grant_valid_bits, o.grant_valid_bits, err_msg=f"grant_valid_bits {what}")
+    np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits, err_msg=f"cert_accept_bits {what}")
+    np.testing.assert_array_equal(g.cert_reason, o.cert_reason, err_msg=f"cert_reason {what}")
+    np.testing.assert_array_equal(g.cert_fail_op, o.cert_fail_op, err_msg=f"cert_fail_op {what}")
+
+
+def test_rsa_public_op_matches_python_pow():
+    pems = W.load_keys(3)
+    mods = [O.pem_modulus(p) for p in pems]
+    ver = mh.Verifier(mods, 0)
+    rng = np.random.default_rng(7)
+    sigs, signer = [], []
+    for i in range(300):
+        k = i % 3
+        N = int.from_bytes(mods[k], "big")
+        kind = i % 6
+        if kind == 0:
+            s = int.from_bytes(O.rsa_sign(pems[k], W.encode_grant(f"k{i}", i, "c" * 128)), "big")
+        elif kind == 1:
+            s = 0
+        elif kind == 2:
+            s = N - 1
+        elif kind == 3:
+            s = int(rng.integers(1, 1 << 62))
+        else:
+            s = int.from_bytes(rng.bytes(256), "big") % N
+        sigs.append(s.to_bytes(256, "big"))
+        signer.append(k)
+    y, z = mh.rsa_public_op(ver, np.frombuffer(b"".join(sigs), np.uint8), np.array(signer), want_z=True)
+    R = 1 << (28 * 74)
+    for i in range(len(sigs)):
+        N = int.from_bytes(mods[signer[i]], "big")
+        s = int.from_bytes(sigs[i], "big")
+        assert int.from_bytes(y[i].tobytes(), "big") == pow(s, 65537, N), i
+        zi = sum(int(v) << (28 * j) for j, v in enumerate(z[i]))
+        assert zi < 2 * N
+        assert zi % N == pow(s, 65536, N) * pow(pow(R, 65535, N), -1, N) % N, i
+    ver.close()
+
+
+def test_rsa_golden_vectors_gpu(golden_dir):
+    d = json.load(open(os.path.join(golden_dir, "rsa_vectors.json")))
+    moduli = [bytes.fromhex(d["moduli"][str(i)]) for i in range(7)]
+    vecs = d["vectors"]
+    msgs = [bytes.fromhex(v["msg"]) for v in vecs]
+    blob = np.frombuffer(b"".join(msgs), np.uint8).copy()
+    off = np.cumsum([0] + [len(m) for m in msgs[:-1]]).astype(np.uint64)
+    n = len(vecs)
+    batch = mh.Batch(
+        grant_bytes=blob, grant_off=off, grant_len=np.array([len(m) for m in msgs], np.uint32),
+        sig=np.frombuffer(b"".join(bytes.fromhex(v["sig"]) for v in vecs), np.uint8).reshape(n, 256).copy(),
+        signer=np.array([v["key"] for v in vecs], np.uint16), grant_key=np.zeros(n, np.uint8),
+        cert_grant_off=np.array([0, n], np.uint32), cert_op_off=np.array([0, 0], np.uint32),
+        op_key=np.zeros(0, np.uint8), op_flags=np.zeros(0, np.uint8), expected_hash=np.zeros((1, 128), np.uint8))
+    ver = mh.Verifier(moduli, 0)
+    g = ver.verify(batch, 4, True)
+    got = (g.grant_flags & mh.GRANT_SIG_OK) != 0
+    want = np.array([v["valid"] for v in vecs])
+    bad = [vecs[i]["name"] for i in np.nonzero(got != want)[0]]
+    assert not bad, bad
+    assert want.sum() == 21
+    ver.close()
+
+
+@pytest.mark.parametrize("key", sorted(grouped_cases().keys()))
+def test_cert_branch_cases_gpu(key):
+    R, strict = key
+    cases = grouped_cases()[key]
+    batch, reason, fail_op = build_case_batch(cases, W.load_keys(R))
+    ver = mh.Verifier(moduli_for(R), 0)
+    g = ver.verify(batch, R, bool(strict))
+    o = O.verify_batch(moduli_for(R), batch, R, bool(strict), 4)
+    assert_same(g, o, str(key))
+    for i, c in enumerate(cases):
+        assert g.cert_reason[i] == reason[i], (c["name"], c["why"])
+        assert g.cert_fail_op[i] == fail_op[i], c["name"]
+    ver.close()
+
+
+@pytest.mark.parametrize("strict", [True, False])
+def test_synthetic_r4_parity(pool4, ver4, strict):
+    s = W.make_batch(pool4, 6000, first_cert=1000)
+    g = ver4.verify(s.batch, 4, strict)
+    o = O.verify_batch(pool4.moduli, s.batch, 4, strict, 8)
+    assert_same(g, o, f"R=4 strict={strict}")
+    np.testing.assert_array_equal(g.grant_flags, s.expected_flags)
+    # every fault class shows up and is judged as the reference would
+    assert set(np.unique(s.fault)) == {0, 1, 2, 3, 4, 5}
+
+
+def test_synthetic_r4_k2_parity(pool4k2):
+    ver = mh.Verifier(pool4k2.moduli, 0)
+    s = W.make_batch(pool4k2, 4000)
+    for strict in (True, False):
+        g = ver.verify(s.batch, 4, strict)
+        o = O.verify_batch(pool4k2.moduli, s.batch, 4, strict, 8)
+        assert_same(g, o, f"k=2 strict={strict}")
+    ver.close()
+
+
+@pytest.mark.parametrize("strict", [True, False])
+def test_synthetic_r7_parity(pool7, ver7, strict):
+    # C3: 7-server certificates; strict = server predicate (> 5, i.e. 6 of 7), else client (>= 5: "5-of-7")
+    s = W.make_batch(pool7, 4000)
+    g = ver7.verify(s.batch, 7, strict)
+    o = O.verify_batch(pool7.moduli, s.batch, 7, strict, 8)
+    assert_same(g, o, f"R=7 strict={strict}")
+    if not strict:
+        # dropped-replica certificates: 6 of 7 valid still reaches 5-of-7
+        drop = s.fault == W.FAULT_DROP
+        assert g.cert_accept[drop].all()
+
+
+def test_large_batch_c2_bit_exact(pool4, ver4):
+    """C2 scale (1M grants, R=4): flags vs ground truth, verdicts vs oracle tally."""
+    C = W.n_certs_for_grants(1_000_000, 4)
+    s = W.make_batch(pool4, C)
+    g = ver4.verify(s.batch, 4, True)
+    np.testing.assert_array_equal(g.grant_flags, s.expected_flags)
+    o = O.tally(s.batch, s.expected_flags, g.grant_ts, 4, True)
+    np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits)
+    np.testing.assert_array_equal(g.cert_reason, o.cert_reason)
+    np.testing.assert_array_equal(g.cert_fail_op, o.cert_fail_op)
+    # ts parsed on device == the oracle's parse on a sample
+    idx = np.arange(0, s.batch.n_grants, 997)
+    for i in idx[:200]:
+        gb = s.batch.grant_bytes[int(s.batch.grant_off[i]):int(s.batch.grant_off[i]) + int(s.batch.grant_len[i])]
+        assert O.grant_parse(gb.tobytes())["timestamp"] == g.grant_ts[i]
+    # the oracle's own signature leg agrees on a sample (independent OpenSSL check)
+    of, ot = O.verify_grants(pool4.moduli, s.batch, 0, 4000, 8)
+    np.testing.assert_array_equal(g.grant_flags[:4000], of[:4000])
+
+
+def test_sig_ge_modulus_rejected(pool4, ver4):
+    s = W.make_batch(pool4, 50, faults=False)
+    b = s.batch
+    N = int.from_bytes(pool4.moduli[int(b.signer[0])], "big")
+    sig0 = int.from_bytes(b.sig[0].tobytes(), "big")
+    if sig0 + N < (1 << 2048):
+        b.sig[0] = np.frombuffer((sig0 + N).to_bytes(256, "big"), np.uint8)  # s + n: same residue, must reject
+    b.sig[1] = np.frombuffer(pool4.moduli[int(b.signer[1])], np.uint8)  # s == n
+    b.sig[2] = 0xFF  # s = 2^2048 - 1 > n
+    g = ver4.verify(b, 4, True)
+    o = O.verify_batch(pool4.moduli, b, 4, True, 2)
+    assert_same(g, o)
+    assert not (g.grant_flags[:3] & 1).any()
+    assert (g.grant_flags[3:] & 1).all()
+
+
+def test_edge_shapes(pool4, ver4):
+    # empty batch
+    empty = mh.Batch(grant_bytes=np.zeros(1, np.uint8), grant_off=np.zeros(0, np.uint64),
+                     grant_len=np.zeros(0, np.uint32), sig=np.zeros((0, 256), np.uint8),
+                     signer=np.zeros(0, np.uint16), grant_key=np.zeros(0, np.uint8),
+                     cert_grant_off=np.zeros(1, np.uint32), cert_op_off=np.zeros(1, np.uint32),
+                     op_key=np.zeros(0, np.uint8), op_flags=np.zeros(0, np.uint8),
+                     expected_hash=np.zeros((0, 128), np.uint8))
+    g = ver4.verify(empty, 4, True)
+    assert g.cert_accept_bits.size == 0
+    # single certificate, single grant; and a batch whose size is not a multiple of 64
+    for C in (1, 3, 17, 65):
+        s = W.make_batch(pool4, C, first_cert=C * 31)
+        g = ver4.verify(s.batch, 4, True)
+        o = O.verify_batch(pool4.moduli, s.batch, 4, True, 2)
+        assert_same(g, o, f"C={C}")
+    # signer index outside the key table -> invalid signature (never verified)
+    s = W.make_batch(pool4, 40, faults=False)
+    s.batch.signer[5] = 4
+    s.batch.signer[9] = 65535
+    g = ver4.verify(s.batch, 4, True)
+    o = O.verify_batch(pool4.moduli, s.batch, 4, True, 2)
+    assert_same(g, o, "bad signer")
+    assert not (g.grant_flags[[5, 9]] & 1).any()
+
+
+def test_long_and_odd_grants(ver4, pool4):
+    """Grants spanning many SHA-256 blocks, empty grants, unaligned offsets."""
+    pems = W.load_keys(4)
+    th = W.txn_hash_hex(5)
+    grants = [W.encode_grant("K" * n, 1000, th) for n in (0, 1, 50, 55, 56, 63, 64, 119, 500, 3000)]
+    grants.append(b"")  # an empty Grant (all defaults) parses fine
+    grants.append(W.encode_grant("K", 1000, th) + b"\x0f")  # malformed
+    blob = bytearray(b"\x01\x02\x03")
+    offs = []
+    for i, gb in enumerate(grants):
+        blob += b"\xaa" * (i % 3)
+        offs.append(len(blob))
+        blob += gb
+    sigs = [O.rsa_sign(pems[i % 4], gb) for i, gb in enumerate(grants)]
+    n = len(grants)
+    b = mh.Batch(grant_bytes=np.frombuffer(bytes(blob), np.uint8).copy(), grant_off=np.array(offs, np.uint64),
+                 grant_len=np.array([len(x) for x in grants], np.uint32),
+                 sig=np.frombuffer(b"".join(sigs), np.uint8).reshape(n, 256).copy(),
+                 signer=np.array([i % 4 for i in range(n)], np.uint16), grant_key=np.zeros(n, np.uint8),
+                 cert_grant_off=np.array([0, 4, 8, n], np.uint32), cert_op_off=np.array([0, 1, 2, 3], np.uint32),
+                 op_key=np.zeros(3, np.uint8), op_flags=np.full(3, 3, np.uint8),
+                 expected_hash=np.stack([np.frombuffer(th.encode(), np.uint8)] * 3))
+    g = ver4.verify(b, 4, False)
+    o = O.verify_batch(pool4.moduli, b, 4, False, 2)
+    assert_same(g, o)
+    assert (g.grant_flags[:n - 1] & 1).all()
+    assert g.grant_flags[n - 1] == 1  # signature fine, bytes unparseable
+    assert g.cert_reason[2] == mh.REJECT_MALFORMED
+
+
+def test_device_resident_path_matches_host_path(pool4, ver4):
+    import torch
+
+    s = W.make_batch(pool4, 3000, first_cert=77)
+    host = ver4.verify(s.batch, 4, True)
+    dev = mh.DeviceBatch(s.batch, 0)
+    out = mh.DeviceVerdicts(dev.n_grants, dev.n_certs, 0)
+    ver4.verify_device(dev, out, 4, True, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    d = out.to_host()
+    assert_same(d, host, "device path")
+
+
+def test_repeatable(pool4, ver4):
+    s = W.make_batch(pool4, 2000, first_cert=5)
+    a = ver4.verify(s.batch, 4, True)
+    b = ver4.verify(s.batch, 4, True)
+    assert_same(a, b, "repeat")
