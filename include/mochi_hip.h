@@ -163,7 +163,7 @@ int mochi_verify_batch(mochi_ctx* ctx, const mochi_batch* batch, const mochi_par
 /*
  * Verify a batch already resident in DEVICE memory (every mochi_batch pointer
  * and every non-NULL mochi_verdicts pointer is a device pointer).  Enqueued on
- * `stream` (a hipStream_t, NULL = the context's stream); asynchronous.  The
+ * `stream` (a hipStream_t; NULL = the null stream, as in every HIP API); asynchronous.  The
  * batch header itself is read on the host.  Scratch is owned by the context.
  */
 int mochi_verify_batch_device(mochi_ctx* ctx, const mochi_batch* batch, const mochi_params* params,
@@ -179,6 +179,16 @@ int mochi_verify_batch_device(mochi_ctx* ctx, const mochi_batch* batch, const mo
  */
 int mochi_rsa_public_op(mochi_ctx* ctx, uint32_t n, const uint8_t* sig_be, const uint16_t* signer, uint8_t* out_be,
                         uint32_t* out_z);
+
+/*
+ * Per-stage device timing.  While profiling is on, every verify call records
+ * hipEvents between its stages on the stream it runs on; mochi_ctx_read_profile
+ * waits for them and returns the SUM over calls since the last read, per stage:
+ * [0] grant prep (parse + SHA-256), [1] signer bucketing, [2] k_rsa_pow,
+ * [3] k_rsa_final (+ bitmap pack), [4] k_tally.  n_stages <= 5.
+ */
+int mochi_ctx_set_profiling(mochi_ctx* ctx, int on);
+int mochi_ctx_read_profile(mochi_ctx* ctx, float* stage_ms, uint32_t n_stages, uint32_t* n_calls);
 
 /* Stream-event timings of the last mochi_verify_batch() call on this context:
  * host->device copy, kernels, device->host copy (milliseconds). */

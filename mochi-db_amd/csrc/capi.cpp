@@ -143,6 +143,9 @@ struct mochi_ctx {
   PinnedBuf pin_in, pin_out;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float last_ms[3] = {0, 0, 0};  // h2d, kernels, d2h of the last host-path call
+  // per-stage profiling (mochi_ctx_set_profiling): one event set per verify call
+  bool profiling = false;
+  std::vector<std::vector<hipEvent_t>> prof_sets;
 };
 
 extern "C" {
@@ -305,6 +308,12 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.cert_accept_bits = o->cert_accept_bits;
   a.cert_reason = o->cert_reason;
   a.cert_fail_op = o->cert_fail_op;
+  if (c->profiling) {
+    std::vector<hipEvent_t> evs(mochi::kProfStages + 1, nullptr);
+    for (auto& e : evs) HIP_TRY(hipEventCreate(&e));
+    c->prof_sets.push_back(evs);
+    a.prof_events = c->prof_sets.back().data();
+  }
   HIP_TRY(mochi::launch_verify(a, st));
   return MOCHI_OK;
 }
@@ -321,7 +330,7 @@ int mochi_verify_batch_device(mochi_ctx* c, const mochi_batch* b, const mochi_pa
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
-  rc = run_device(c, b, p, o, stream ? (hipStream_t)stream : c->stream);
+  rc = run_device(c, b, p, o, (hipStream_t)stream);  // NULL = the null stream, as in HIP
   (void)hipSetDevice(save);
   return rc;
 }
@@ -505,6 +514,33 @@ int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const u
       if (g == 0xFFFFFFFFu) continue;
       for (int j = 0; j < mochi::kL; j++) out_z[(size_t)g * mochi::kL + j] = z[(size_t)j * slots + sl];
     }
+  return MOCHI_OK;
+}
+
+int mochi_ctx_set_profiling(mochi_ctx* c, int on) {
+  if (!c) return fail(MOCHI_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->profiling = on != 0;
+  return MOCHI_OK;
+}
+
+int mochi_ctx_read_profile(mochi_ctx* c, float* stage_ms, uint32_t n_stages, uint32_t* n_calls) {
+  if (!c || !stage_ms) return fail(MOCHI_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (uint32_t i = 0; i < n_stages; i++) stage_ms[i] = 0.f;
+  uint32_t calls = 0;
+  for (auto& evs : c->prof_sets) {
+    if (hipEventSynchronize(evs.back()) != hipSuccess) return fail(MOCHI_EHIP, "hipEventSynchronize failed");
+    for (uint32_t i = 0; i < n_stages && i < (uint32_t)mochi::kProfStages; i++) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, evs[i], evs[i + 1]);
+      stage_ms[i] += ms;
+    }
+    for (auto e : evs) (void)hipEventDestroy(e);
+    calls++;
+  }
+  c->prof_sets.clear();
+  if (n_calls) *n_calls = calls;
   return MOCHI_OK;
 }
 

@@ -43,7 +43,12 @@ struct LaunchArgs {
   // mochi_rsa_public_op only: raw s^65537 mod n words [N][64] (else null)
   uint32_t* dbg_y;
   bool skip_prep_tally;
+  // optional per-stage timing: kProfStages + 1 events recorded on the launch stream
+  hipEvent_t* prof_events;
 };
+
+// Stages timed when LaunchArgs::prof_events is set.
+enum ProfStage { kStagePrep = 0, kStageBucket, kStagePow, kStageFinal, kStageTally, kProfStages };
 
 // Slots of the signer-bucketed RSA grid: every bucket is padded to 64.
 inline uint64_t slot_capacity(uint32_t n_grants, uint32_t n_keys) {

@@ -479,10 +479,15 @@ static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b -
 
 hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   const uint32_t N = a.n_grants, C = a.n_certs;
-  if (N) {
-    if (!a.skip_prep_tally)
+  auto mark = [&](int i) {
+    if (a.prof_events) (void)hipEventRecord(a.prof_events[i], st);
+  };
+  mark(0);
+  if (N && !a.skip_prep_tally)
     hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, st, a.blob, a.grant_off, a.grant_len, N,
                        a.digest, a.ts, nullptr, a.hash_off, a.hash_len, a.flags);
+  mark(1 + kStagePrep);
+  if (N) {
     hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, st);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(a.perm, 0xFF, sizeof(uint32_t) * (size_t)a.n_slots, st);
@@ -493,16 +498,22 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, a.count, a.n_keys, a.cursor, a.total);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(cdiv(N, 256)), dim3(256), 2 * lds, st, a.signer, N, a.n_keys, a.cursor,
                        a.perm);
-    launch_rsa_pow(a, st);
+  }
+  mark(1 + kStageBucket);
+  if (N) launch_rsa_pow(a, st);
+  mark(1 + kStagePow);
+  if (N) {
     launch_rsa_final(a, st);
     if (a.grant_valid_bits)
       hipLaunchKernelGGL(k_pack_bits, dim3(cdiv(N, 256)), dim3(256), 0, st, a.flags, N, (uint8_t)MOCHI_GRANT_SIG_OK,
                          a.grant_valid_bits);
   }
+  mark(1 + kStageFinal);
   if (C && !a.skip_prep_tally)
     hipLaunchKernelGGL(k_tally, dim3(cdiv(C, 256)), dim3(256), 0, st, a.cert_grant_off, a.cert_op_off, a.grant_key,
                        a.op_key, a.op_flags, a.flags, a.ts, a.blob, a.hash_off, a.hash_len, a.expected_hash, C,
                        a.majority, a.strict_gt, a.cert_accept_bits, a.cert_reason, a.cert_fail_op);
+  mark(1 + kStageTally);
   return hipGetLastError();
 }
 

@@ -110,6 +110,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise MochiError(f"{path} not built: run `make -C mochi-db_amd` (or __graft_entry__.build())")
+    # One HIP runtime per process: when PyTorch-ROCm is present, load it first so
+    # that libmochi_hip's libamdhip64.so.7 dependency resolves (by SONAME) to the
+    # runtime torch already mapped; device pointers and hipStream_t handles can
+    # then cross the boundary.  Loading ours first would make torch map a second
+    # runtime, which then sees no GPU.
+    try:
+        import torch  # noqa: F401  (plumbing only)
+    except Exception:
+        pass
     lib = ctypes.CDLL(path)
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32
     lib.mochi_abi_version.restype = ctypes.c_int
@@ -126,6 +135,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_sign_grants.argtypes = [ctypes.c_char_p, u32, vp, vp, vp, vp, ctypes.c_int]
     lib.mochi_pem_modulus.argtypes = [ctypes.c_char_p, vp]
     lib.mochi_rsa_public_op.argtypes = [vp, u32, vp, vp, vp, vp]
+    lib.mochi_ctx_set_profiling.argtypes = [vp, ctypes.c_int]
+    lib.mochi_ctx_read_profile.argtypes = [vp, vp, u32, vp]
     lib.mochi_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
     if lib.mochi_abi_version() != 1:
         raise MochiError("libmochi_hip ABI mismatch")
@@ -302,6 +313,23 @@ class Verifier:
         h, k, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
         self.lib.mochi_ctx_last_timing(self.ctx, ctypes.byref(h), ctypes.byref(k), ctypes.byref(d))
         out.timing_ms = {"h2d": h.value, "kernels": k.value, "d2h": d.value}
+        return out
+
+    STAGES = ("prep_sha256", "bucket", "rsa_pow", "rsa_final", "tally")
+
+    def set_profiling(self, on: bool) -> None:
+        self.lib.mochi_ctx_set_profiling(self.ctx, 1 if on else 0)
+
+    def read_profile(self) -> dict:
+        """Mean per-call stage times (ms) since the last read; waits for the device."""
+        arr = (ctypes.c_float * len(self.STAGES))()
+        n = ctypes.c_uint32()
+        rc = self.lib.mochi_ctx_read_profile(self.ctx, arr, len(self.STAGES), ctypes.byref(n))
+        if rc != OK:
+            raise MochiError(f"mochi_ctx_read_profile rc={rc}: {_err(self.lib)}")
+        calls = max(1, n.value)
+        out = {name: arr[i] / calls for i, name in enumerate(self.STAGES)}
+        out["calls"] = n.value
         return out
 
     def verify_device(self, dev: "DeviceBatch", out: "DeviceVerdicts", replication_factor: int,

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""CPU baseline for bench.py: the oracle verifier timed on this host's cores.
+
+Runs as its own process (bench.py starts it with subprocess before touching
+the GPU), so its worker processes are forked from a process that never
+initialised HIP.  OpenSSL 3.0 serialises threads of one process on shared
+provider state (8 threads: ~1.4x one thread here), so the grant signatures are
+split over worker PROCESSES, as `openssl speed -multi` does; the certificate
+tally (restated InMemoryDataStore.java:576-640) then runs in the parent and is
+included in the timed region.
+
+Prints one JSON object; with --flags-out also saves the grant flags / reasons
+so bench.py can check them against the GPU's verdicts for the same grants.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mochi-db_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+_G = {}
+
+
+def _work(rng):
+    import oracle_ffi as O
+
+    b, e = rng
+    flags, ts = O.verify_grants(_G["moduli"], _G["batch"], b, e, 1)
+    return b, e, flags[b:e].copy(), ts[b:e].copy()
+
+
+def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=None):
+    import numpy as np
+
+    import oracle_ffi as O
+    import workload as W
+
+    pool = W.build_pool(R=R, k=k, P=pool_size, P_f=256, cache_dir=cache_dir)
+    # calibrate: one process, a few hundred grants
+    probe = W.make_batch(pool, 256)
+    t0 = time.perf_counter()
+    O.verify_grants(pool.moduli, probe.batch, 0, probe.batch.n_grants, 1)
+    rate1 = probe.batch.n_grants / max(1e-6, time.perf_counter() - t0)
+    want = int(rate1 * procs * seconds / (R * k))
+    n = max(64, min(n_certs, want))
+    s = W.make_batch(pool, n)
+    N = s.batch.n_grants
+    _G["moduli"], _G["batch"] = pool.moduli, s.batch.normalized()
+    chunks = max(procs * 4, 1)
+    ranges = [(N * i // chunks, N * (i + 1) // chunks) for i in range(chunks)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as p:
+        p.map(_work, ranges[:procs])  # warm the workers (library load, key setup)
+        t0 = time.perf_counter()
+        flags = np.zeros(N, np.uint8)
+        ts = np.zeros(N, np.int64)
+        for b, e, f, t in p.imap_unordered(_work, ranges):
+            flags[b:e] = f
+            ts[b:e] = t
+        v = O.tally(s.batch, flags, ts, R, strict)
+        dt = time.perf_counter() - t0
+    if flags_out:
+        np.savez(flags_out, grant_flags=flags, cert_reason=v.cert_reason, cert_accept_bits=v.cert_accept_bits)
+    cpu = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(N / dt, 1),
+        "unit": "grants/s",
+        "cores": procs,
+        "kind": "port",
+        "sample": f"first {n} certificates ({N} grants) of the C2 stream; OpenSSL 3.0.2 SHA-256 + RSA-2048 PKCS#1 "
+                  f"v1.5 verify per grant + restated InMemoryDataStore.java:576-640 tally; {procs} worker processes "
+                  f"on '{cpu}'; {dt:.1f} s",
+        "single_core_grants_per_s": round(rate1, 1),
+        "n_certs": n,
+        "n_grants": N,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--replication", type=int, default=4)
+    ap.add_argument("--ops-per-txn", type=int, default=1)
+    ap.add_argument("--pool", type=int, default=4096)
+    ap.add_argument("--cache-dir", default="/tmp/mochi_bench_cache")
+    ap.add_argument("--max-certs", type=int, default=250_000)
+    ap.add_argument("--procs", type=int, default=0)
+    ap.add_argument("--seconds", type=float, default=12.0)
+    ap.add_argument("--client-predicate", action="store_true")
+    ap.add_argument("--flags-out", default=None)
+    a = ap.parse_args()
+    procs = a.procs or max(1, min(16, len(os.sched_getaffinity(0))))
+    res = run(a.replication, a.ops_per_txn, a.pool, a.cache_dir, a.max_certs, procs, a.seconds,
+              not a.client_predicate, a.flags_out)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
