@@ -101,14 +101,13 @@ def main():
     dev = mh.DeviceBatch(batch, local_rank)
     out = mh.DeviceVerdicts(dev.n_grants, dev.n_certs, local_rank, full=True)
     stream = torch.cuda.current_stream()
-    gathered = None
-    if dist is not None:
-        gathered = torch.empty(world * out.cert_accept_bits.numel(), dtype=torch.int32, device=out.cert_accept_bits.device)
+    import shard
 
     def step():
         ver.verify_device(dev, out, R, strict, stream=stream.cuda_stream)
-        if dist is not None:
-            dist.all_gather_into_tensor(gathered, out.cert_accept_bits)
+        if dist is not None:  # the only collective: RCCL all-gather of the verdict bitmaps
+            return shard.allgather_bitmaps(out.cert_accept_bits, world)
+        return out.cert_accept_bits
 
     for _ in range(args.warmup):
         step()
