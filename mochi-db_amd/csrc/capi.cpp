@@ -105,26 +105,43 @@ int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
   uint32_t inv = 1;
   for (int i = 0; i < 6; i++) inv *= 2u - e->n32[0] * inv;
   e->n0inv = (0u - inv) & kLimbMask;
-  // kfix = R^65537 mod n, R = 2^(28*74)
+  // Per-key constants (R = 2^(28*74)):
+  //   kfix = R^65537 mod n                       (k_rsa_raw: z*K*s = s^65537)
+  //   q    = R^-(2^16) mod n                     (k_rsa_final: MontMul(z, s) = s^65537 * q)
+  //   a2   = (Cpad * q mod n) + 2n               (k_rsa_final: target EM*q = Cpad*q + H*q)
+  // Cpad = EMSA-PKCS1-v1_5 encoding (RFC 8017 §9.2) of SHA-256 with an all-zero digest.
+  uint8_t cpad[256];
+  memset(cpad, 0xFF, sizeof cpad);
+  static const uint8_t kDigestInfo[19] = {0x30, 0x31, 0x30, 0x0d, 0x06, 0x09, 0x60, 0x86, 0x48, 0x01,
+                                          0x65, 0x03, 0x04, 0x02, 0x01, 0x05, 0x00, 0x04, 0x20};
+  cpad[0] = 0x00;
+  cpad[1] = 0x01;
+  cpad[256 - 32 - 19 - 1] = 0x00;
+  memcpy(cpad + 256 - 32 - 19, kDigestInfo, 19);
+  memset(cpad + 256 - 32, 0, 32);
   BN_CTX* ctx = BN_CTX_new();
-  BIGNUM *n = BN_bin2bn(n_be, 256, nullptr), *r = BN_new(), *k = BN_new(), *ex = BN_new();
-  int ok = ctx && n && r && k && ex;
+  BIGNUM *n = BN_bin2bn(n_be, 256, nullptr), *r = BN_new(), *k = BN_new(), *ex = BN_new(), *t = BN_new(),
+         *q = BN_new(), *a2 = BN_new(), *cp = BN_bin2bn(cpad, 256, nullptr), *n2 = BN_new();
+  int ok = ctx && n && r && k && ex && t && q && a2 && cp && n2;
   ok = ok && BN_set_bit(r, kL * kLimbBits) && BN_mod(r, r, n, ctx);
   ok = ok && BN_set_word(ex, MOCHI_RSA_E) && BN_mod_exp(k, r, ex, n, ctx);
-  uint8_t kbe[256];
-  ok = ok && BN_bn2binpad(k, kbe, 256) == 256;
-  BN_free(n);
-  BN_free(r);
-  BN_free(k);
-  BN_free(ex);
+  ok = ok && BN_set_word(ex, 1u << 16) && BN_mod_exp(t, r, ex, n, ctx) && BN_mod_inverse(q, t, n, ctx) != nullptr;
+  ok = ok && BN_mod_mul(a2, cp, q, n, ctx) && BN_lshift1(n2, n) && BN_add(a2, a2, n2);
+  auto to_limbs_bn = [](const BIGNUM* v, uint32_t* x) {
+    uint8_t le[264];
+    if (BN_bn2lebinpad(v, le, sizeof le) != (int)sizeof le) return 0;
+    for (int j = 0; j < kL; j++) {
+      const int bit = j * kLimbBits, by = bit >> 3, sh = bit & 7;
+      uint64_t w = 0;
+      for (int b = 0; b < 5; b++) w |= (uint64_t)le[by + b] << (8 * b);
+      x[j] = (uint32_t)(w >> sh) & kLimbMask;
+    }
+    return 1;
+  };
+  ok = ok && to_limbs_bn(k, e->kfix) && to_limbs_bn(q, e->q) && to_limbs_bn(a2, e->a2);
+  for (BIGNUM* b : {n, r, k, ex, t, q, a2, cp, n2}) BN_free(b);
   BN_CTX_free(ctx);
   if (!ok) return fail(MOCHI_EINVAL, "key precompute failed");
-  uint32_t kw[64];
-  for (int i = 0; i < 64; i++) {
-    const uint8_t* b = kbe + 256 - 4 * (i + 1);
-    kw[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
-  }
-  to_limbs(kw, e->kfix);
   return MOCHI_OK;
 }
 

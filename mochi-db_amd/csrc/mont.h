@@ -28,12 +28,14 @@ constexpr int kL = 74;  // 74 * 28 = 2072 bits
 // Per-key device table entry (uploaded once per context).
 struct KeyEntry {
   uint32_t n[kL];     // modulus, 28-bit limbs, little-endian limb order
-  uint32_t kfix[kL];  // R^65537 mod n (R = 2^2072): undoes the R^-(2^16-1) of the squaring chain
+  uint32_t kfix[kL];  // R^65537 mod n (R = 2^2072): undoes the R^-(2^16-1) of the squaring chain (k_rsa_raw)
+  uint32_t q[kL];     // Q = R^-(2^16) mod n: the verify target is EM * Q (k_rsa_final)
+  uint32_t a2[kL];    // (Cpad * Q mod n) + 2n, Cpad = EM with a zero digest (k_rsa_final)
   uint32_t n0inv;     // -n^{-1} mod 2^28
   uint32_t n32[64];   // modulus as 32-bit words, little-endian word order
-  uint32_t pad[11];   // 74+74+1+64+11 = 224 words = 896 bytes
+  uint32_t pad[7];    // 4*74+1+64+7 = 368 words = 1472 bytes
 };
-static_assert(sizeof(KeyEntry) == 896, "KeyEntry layout");
+static_assert(sizeof(KeyEntry) == 1472, "KeyEntry layout");
 
 // Wave-uniform table reads go through the constant address space so the
 // compiler emits scalar loads (SGPR operands for v_mad_u64_u32).
