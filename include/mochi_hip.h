@@ -224,6 +224,40 @@ int mochi_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const u
                           const uint64_t* chosen_off, uint32_t replication_factor, int32_t* chosen,
                           uint8_t* reason, uint32_t* accept_bits);
 
+/* Write1 response kinds: the ProtocolMessage payload case a Write1ToServer got
+ * back (MochiDBClient.java:274-289). */
+#define MOCHI_W1_OK 0             /* WRITE1OKFROMSERVER                        */
+#define MOCHI_W1_REFUSED 1        /* WRITE1REFUSEDFROMSERVER                   */
+#define MOCHI_W1_REQUEST_FAILED 2 /* REQUESTFAILEDFROMSERVER                   */
+#define MOCHI_W1_OTHER 3          /* any other payload                         */
+
+/* Write1 round outcomes (MochiDBClient.executeWriteTransactionBL). */
+enum mochi_write1_decision {
+  MOCHI_W1_PROCEED = 0,           /* every response OK, timestamps uniform -> Write2 (:320-324)      */
+  MOCHI_W1_RETRY = 1,             /* OK multigrants disagree on a key's timestamp -> sleep 1 ms and
+                                     resend Write1 (isUniformTimeStampInMultiGrants, :195-219, :310-318) */
+  MOCHI_W1_THROW_REFUSED = 2,     /* RequestRefusedException (:325-328)                              */
+  MOCHI_W1_THROW_FAILED = 3,      /* RequestFailedException (:281-283)                               */
+  MOCHI_W1_THROW_UNSUPPORTED = 4, /* a WRONG_SHARD grant in an OK/REFUSED multigrant:
+                                     removeWrongShardGrantFromMultiGrant removes from protobuf's
+                                     read-only map view -> UnsupportedOperationException (:221-228) */
+};
+
+/*
+ * Client Write1 round classification (a8 + a9), batched over requests.
+ * Request r owns responses [resp_off[r], resp_off[r+1]) in arrival order;
+ * response q has payload kind resp_kind[q] (MOCHI_W1_*), the replying
+ * MultiGrant.serverId as a small integer resp_server[q], and grants
+ * [resp_grant_off[q], resp_grant_off[q+1]) (CSR over all responses).  Grant g:
+ * grant_key[g] = slot of its objectId among the transaction's op keys (0xFF if
+ * it is no op's key), grant_ts[g] = Grant.timestamp, grant_status[g] =
+ * OperationResultStatus (0 OK, 1 WRONG_SHARD).  decision[r] receives an enum
+ * mochi_write1_decision.  Host memory; pure CPU.
+ */
+int mochi_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const uint8_t* resp_kind,
+                          const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
+                          const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision);
+
 #ifdef __cplusplus
 }
 #endif

@@ -606,4 +606,60 @@ int mochi_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const u
   return MOCHI_OK;
 }
 
+int mochi_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const uint8_t* resp_kind,
+                          const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
+                          const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision) {
+  if (!resp_off || !resp_kind || !resp_server || !resp_grant_off || !decision)
+    return fail(MOCHI_EINVAL, "null argument");
+  if (resp_grant_off[resp_off[n_requests]] > resp_grant_off[0] && (!grant_key || !grant_ts || !grant_status))
+    return fail(MOCHI_EINVAL, "null grant arrays");
+  std::vector<uint32_t> ok_servers;
+  for (uint32_t r = 0; r < n_requests; r++) {
+    const uint32_t q0 = resp_off[r], q1 = resp_off[r + 1];
+    if (q1 < q0) return fail(MOCHI_EINVAL, "resp_off not monotone at request %u", r);
+    // one pass: REQUESTFAILED dominates, then any WRONG_SHARD grant in an OK/REFUSED multigrant
+    bool failed = false, wrong_shard = false, all_ok = true;
+    for (uint32_t q = q0; q < q1; q++) {
+      const uint8_t kind = resp_kind[q];
+      all_ok &= kind == MOCHI_W1_OK;
+      failed |= kind == MOCHI_W1_REQUEST_FAILED;
+      if (kind == MOCHI_W1_OK || kind == MOCHI_W1_REFUSED)
+        for (uint32_t g = resp_grant_off[q]; g < resp_grant_off[q + 1]; g++) wrong_shard |= grant_status[g] == 1;
+    }
+    uint8_t d;
+    if (failed) d = MOCHI_W1_THROW_FAILED;
+    else if (wrong_shard) d = MOCHI_W1_THROW_UNSUPPORTED;
+    else {
+      // uniformity over the surviving OK multigrant of every serverId (the
+      // last one, HashMap.put): walk backwards, skip ids already taken
+      int64_t ts0[256];
+      uint8_t seen[256];
+      memset(seen, 0, sizeof seen);
+      ok_servers.clear();
+      bool uniform = true;
+      for (uint32_t q = q1; q-- > q0 && uniform;) {
+        if (resp_kind[q] != MOCHI_W1_OK) continue;
+        bool dup = false;
+        for (uint32_t sid : ok_servers) dup |= sid == resp_server[q];
+        if (dup) continue;
+        ok_servers.push_back(resp_server[q]);
+        for (uint32_t g = resp_grant_off[q]; g < resp_grant_off[q + 1]; g++) {
+          const uint8_t k = grant_key[g];
+          if (k == 0xFF) continue;
+          if (!seen[k]) {
+            seen[k] = 1;
+            ts0[k] = grant_ts[g];
+          } else if (ts0[k] != grant_ts[g]) {
+            uniform = false;
+            break;
+          }
+        }
+      }
+      d = !uniform ? MOCHI_W1_RETRY : all_ok ? MOCHI_W1_PROCEED : MOCHI_W1_THROW_REFUSED;
+    }
+    decision[r] = d;
+  }
+  return MOCHI_OK;
+}
+
 }  // extern "C"

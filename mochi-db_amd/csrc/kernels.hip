@@ -81,7 +81,12 @@ __device__ bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
   while (i < n) {
     const uint32_t c = r.at(off + i);
     if (c < 0x80) {
-      i++;
+      // ASCII fast path: skip every remaining byte of the cached word when all
+      // of them are ASCII and inside the string (keys and the 128-char hex
+      // transactionHash are ASCII, so this is 4 bytes per step)
+      const uint32_t sub = (off + i + r.shift) & 3, rest = 4 - sub;
+      if (i + rest <= n && ((r.w >> (8 * sub)) & (0x80808080u >> (8 * sub))) == 0) i += rest;
+      else i++;
       continue;
     }
     if (c < 0xC2) return false;

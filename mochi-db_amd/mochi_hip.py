@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_ctx_set_profiling.argtypes = [vp, ctypes.c_int]
     lib.mochi_ctx_read_profile.argtypes = [vp, vp, u32, vp]
     lib.mochi_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
+    lib.mochi_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
     if lib.mochi_abi_version() != 1:
         raise MochiError("libmochi_hip ABI mismatch")
     _lib = lib
@@ -485,3 +486,40 @@ def tally_responses(responses: Sequence[Sequence[Sequence[int]]], n_ops: Sequenc
     acc = unpack_bits(bits, nreq)
     ch = [chosen[int(chosen_off[r]):int(chosen_off[r]) + n_ops[r]].copy() for r in range(nreq)]
     return acc, reason[:nreq].copy(), ch
+
+
+# Write1 response kinds / round decisions (include/mochi_hip.h)
+W1_OK, W1_REFUSED, W1_REQUEST_FAILED, W1_OTHER = 0, 1, 2, 3
+W1_PROCEED, W1_RETRY, W1_THROW_REFUSED, W1_THROW_FAILED, W1_THROW_UNSUPPORTED = 0, 1, 2, 3, 4
+
+
+def pack_write1(requests):
+    """requests[r] = list of responses (kind, server_id, [(key_slot, ts, status), ...])
+    -> the CSR arrays of mochi_write1_classify."""
+    resp_off = np.zeros(len(requests) + 1, np.uint32)
+    kinds, servers, goff, keys, tss, sts = [], [], [0], [], [], []
+    for r, resps in enumerate(requests):
+        resp_off[r + 1] = resp_off[r] + len(resps)
+        for kind, sid, grants in resps:
+            kinds.append(kind)
+            servers.append(sid)
+            for key, ts, st in grants:
+                keys.append(key)
+                tss.append(ts)
+                sts.append(st)
+            goff.append(len(keys))
+    arr = lambda v, dt: np.asarray(v if v else [0], dt)
+    return (resp_off, arr(kinds, np.uint8), arr(servers, np.uint32), np.asarray(goff, np.uint32),
+            arr(keys, np.uint8), arr(tss, np.int64), arr(sts, np.uint8))
+
+
+def write1_classify(requests) -> np.ndarray:
+    """Client Write1 round outcome per request (MochiDBClient.java:236-332) via libmochi_hip."""
+    lib = load_library()
+    a = pack_write1(requests)
+    out = np.zeros(max(len(requests), 1), np.uint8)
+    rc = lib.mochi_write1_classify(len(requests), *[_ptr(x) for x in a], _ptr(out))
+    if rc != OK:
+        raise MochiError(f"mochi_write1_classify: {_err(lib)}")
+    return out[:len(requests)].copy()
+

@@ -598,6 +598,65 @@ int oracle_write1_uniform(uint32_t n_grants, const uint8_t* grant_key, const int
 }
 
 /* ------------------------------------------------------------------------ */
+/* a8 + a9: client Write1 round — MochiDBClient.java:236-332                   */
+/* ------------------------------------------------------------------------ */
+int oracle_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const uint8_t* resp_kind,
+                           const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
+                           const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision) {
+  if (!resp_off || !resp_kind || !resp_server || !resp_grant_off || !decision) return MOCHI_EINVAL;
+  for (uint32_t r = 0; r < n_requests; r++) {
+    const uint32_t q0 = resp_off[r], q1 = resp_off[r + 1];
+    int all_ok = 1, d = -1;
+    /* :274-290 response loop: REQUESTFAILED throws on the spot */
+    for (uint32_t q = q0; q < q1; q++) {
+      if (resp_kind[q] != MOCHI_W1_OK) all_ok = 0;
+      if (resp_kind[q] == MOCHI_W1_REQUEST_FAILED) {
+        d = MOCHI_W1_THROW_FAILED; /* :281-283 */
+        break;
+      }
+    }
+    /* :295-307 multigrant maps; removeWrongShardGrantFromMultiGrant removes from
+     * the read-only protobuf map view -> UnsupportedOperationException (:221-228) */
+    for (uint32_t q = q0; q < q1 && d < 0; q++) {
+      if (resp_kind[q] != MOCHI_W1_OK && resp_kind[q] != MOCHI_W1_REFUSED) continue;
+      for (uint32_t g = resp_grant_off[q]; g < resp_grant_off[q + 1]; g++)
+        if (grant_status[g] == 1 /* WRONG_SHARD */) {
+          d = MOCHI_W1_THROW_UNSUPPORTED;
+          break;
+        }
+    }
+    if (d < 0) {
+      /* :310 isUniformTimeStampInMultiGrants over write1mutiGrants: one entry per
+       * serverId, the last OK response with that id wins (HashMap.put, :299) */
+      int seen[256] = {0};
+      int64_t ts0[256];
+      int uniform = 1;
+      for (uint32_t q = q0; q < q1 && uniform; q++) {
+        if (resp_kind[q] != MOCHI_W1_OK) continue;
+        int superseded = 0;
+        for (uint32_t p = q + 1; p < q1; p++)
+          if (resp_kind[p] == MOCHI_W1_OK && resp_server[p] == resp_server[q]) superseded = 1;
+        if (superseded) continue;
+        for (uint32_t g = resp_grant_off[q]; g < resp_grant_off[q + 1] && uniform; g++) {
+          const uint8_t k = grant_key[g];
+          if (k == 0xFF) continue; /* allGrants.get(op.getOperand1()) never reaches it :202-205 */
+          if (!seen[k]) {
+            seen[k] = 1;
+            ts0[k] = grant_ts[g]; /* :212-214 */
+          } else if (ts0[k] != grant_ts[g]) {
+            uniform = 0; /* :208-210 */
+          }
+        }
+      }
+      if (!uniform) d = MOCHI_W1_RETRY;                          /* :310-318 */
+      else d = all_ok ? MOCHI_W1_PROCEED : MOCHI_W1_THROW_REFUSED; /* :320-328 */
+    }
+    decision[r] = (uint8_t)d;
+  }
+  return MOCHI_OK;
+}
+
+/* ------------------------------------------------------------------------ */
 /* a10: client Read / Write2 aggregation — MochiDBClient.java:148-175, 355-382 */
 /* ------------------------------------------------------------------------ */
 int oracle_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const uint32_t* n_ops,

@@ -93,6 +93,14 @@ int oracle_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const 
  * grant_key[i] = op key slot, ts[i] = timestamp.  Returns 1 uniform, 0 not. */
 int oracle_write1_uniform(uint32_t n_grants, const uint8_t* grant_key, const int64_t* ts);
 
+/* Client Write1 round classification restated (MochiDBClient.java:236-332,
+ * with isUniformTimeStampInMultiGrants :195-219 and
+ * removeWrongShardGrantFromMultiGrant :221-235); same contract as
+ * mochi_write1_classify. */
+int oracle_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const uint8_t* resp_kind,
+                           const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
+                           const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision);
+
 /* --- fixture generation helpers (tests only) --- */
 
 /* Sign SHA-256(msg) with a PEM RSA private key (PKCS#1 v1.5).  Returns 1 ok. */

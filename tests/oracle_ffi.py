@@ -42,6 +42,7 @@ def lib():
         L.oracle_tally.argtypes = [vp, vp, vp, vp, vp]
         L.oracle_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
         L.oracle_write1_uniform.argtypes = [u32, vp, vp]
+        L.oracle_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_rsa_sign.argtypes = [ctypes.c_char_p, vp, sz, vp]
         L.oracle_pem_modulus.argtypes = [ctypes.c_char_p, vp]
         _lib = L
@@ -194,3 +195,15 @@ def tally_responses(responses, n_ops, replication_factor: int):
     acc = np.unpackbits(bits.view(np.uint8), bitorder="little")[:nreq].astype(bool)
     ch = [chosen[int(chosen_off[r]):int(chosen_off[r]) + n_ops[r]].copy() for r in range(nreq)]
     return acc, reason[:nreq].copy(), ch
+
+
+def write1_classify(requests):
+    """Oracle restatement of the client Write1 round (same packing as mochi_hip.pack_write1)."""
+    import mochi_hip as mh
+
+    a = mh.pack_write1(requests)
+    out = np.zeros(max(len(requests), 1), np.uint8)
+    rc = lib().oracle_write1_classify(len(requests), *[x.ctypes.data for x in a], out.ctypes.data)
+    assert rc == 0
+    return out[:len(requests)].copy()
+

@@ -102,3 +102,60 @@ def test_client_tally_reference_semantics():
     # op-count mismatch -> InconsistentReadException path
     acc, why, _ = mh.tally_responses([[[0, 0], [0]]], [2], 4)
     assert not acc[0] and why[0] == 1
+
+
+def _random_write1(rng, n):
+    reqs = []
+    for _ in range(n):
+        R = int(rng.integers(1, 8))
+        k = int(rng.integers(1, 4))
+        base = rng.integers(0, 5, size=k) * 1000
+        resps = []
+        for q in range(R):
+            u = rng.random()
+            kind = mh.W1_OK if u < 0.85 else mh.W1_REFUSED if u < 0.93 else mh.W1_REQUEST_FAILED if u < 0.97 else mh.W1_OTHER
+            sid = q if rng.random() > 0.05 else int(rng.integers(0, R))  # occasional duplicate serverId
+            grants = []
+            for j in range(k):
+                if rng.random() < 0.05:
+                    continue
+                ts = int(base[j] + (1 if rng.random() < 0.08 else 0))
+                st = 1 if rng.random() < 0.01 else 0
+                grants.append((j, ts, st))
+            if rng.random() < 0.1:
+                grants.append((0xFF, int(rng.integers(0, 9999)), 0))  # a grant for no op key
+            resps.append((kind, sid, grants))
+        reqs.append(resps)
+    return reqs
+
+
+def test_write1_classify_matches_oracle():
+    rng = np.random.default_rng(77)
+    reqs = _random_write1(rng, 3000)
+    got = mh.write1_classify(reqs)
+    exp = O.write1_classify(reqs)
+    assert np.array_equal(got, exp)
+    assert set(np.unique(got).tolist()) == {0, 1, 2, 3, 4}
+
+
+def test_write1_classify_reference_semantics():
+    ok = lambda sid, g: (mh.W1_OK, sid, g)
+    # all OK, uniform -> Write2 (MochiDBClient.java:320-324)
+    assert mh.write1_classify([[ok(0, [(0, 5, 0)]), ok(1, [(0, 5, 0)])]])[0] == mh.W1_PROCEED
+    # non-uniform -> retry (:310-318), even when another server refused
+    assert mh.write1_classify([[ok(0, [(0, 5, 0)]), ok(1, [(0, 6, 0)]),
+                                (mh.W1_REFUSED, 2, [(0, 9, 0)])]])[0] == mh.W1_RETRY
+    # refused grants are not part of the uniformity check -> RequestRefusedException (:325-328)
+    assert mh.write1_classify([[ok(0, [(0, 5, 0)]), (mh.W1_REFUSED, 1, [(0, 9, 0)])]])[0] == mh.W1_THROW_REFUSED
+    # REQUESTFAILED anywhere throws first (:281-283)
+    assert mh.write1_classify([[ok(0, [(0, 5, 0)]), ok(1, [(0, 6, 0)]),
+                                (mh.W1_REQUEST_FAILED, 2, [])]])[0] == mh.W1_THROW_FAILED
+    # a WRONG_SHARD grant -> removal from the read-only map view throws (:221-228)
+    assert mh.write1_classify([[ok(0, [(0, 5, 1)])]])[0] == mh.W1_THROW_UNSUPPORTED
+    # a later OK response with the same serverId replaces the earlier one (HashMap.put, :299)
+    assert mh.write1_classify([[ok(0, [(0, 5, 0)]), ok(1, [(0, 6, 0)]), ok(0, [(0, 6, 0)])]])[0] == mh.W1_PROCEED
+    # grants for keys outside the transaction are never consulted (:202-205)
+    assert mh.write1_classify([[ok(0, [(0, 5, 0), (0xFF, 1, 0)]), ok(1, [(0, 5, 0), (0xFF, 2, 0)])]])[0] == mh.W1_PROCEED
+    # OTHER payloads clear allWriteOk only (:284-287)
+    assert mh.write1_classify([[ok(0, [(0, 5, 0)]), (mh.W1_OTHER, 1, [])]])[0] == mh.W1_THROW_REFUSED
+
