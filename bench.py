@@ -165,8 +165,7 @@ def main():
             cpu["agrees_with_gpu"] = bool(np.array_equal(z["grant_flags"], host.grant_flags[:n]) and
                                           np.array_equal(z["cert_reason"], host.cert_reason[:z["cert_reason"].shape[0]]))
         # PCIe-inclusive host path (never the headline value)
-        hv = ver.verify(batch, R, strict)
-        host_ms = sum(hv.timing_ms.values())
+        host = host_path(ver, batch, R, strict)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -205,7 +204,8 @@ def main():
             "stage_ms": {"prep_sha256": round(stage_ms[0], 4), "bucket": round(stage_ms[1], 4),
                          "rsa_pow": round(stage_ms[2], 4), "rsa_final": round(stage_ms[3], 4),
                          "tally": round(stage_ms[4], 4)},
-            "host_path_pcie_inclusive_grants_per_s": round(N / (host_ms / 1e3), 1) if host_ms > 0 else None,
+            "host_path_pcie_inclusive_grants_per_s": host["pinned_grants_per_s"],
+            "host_path": host,
             "correct_vs_ground_truth": all_ok,
             "cpu_baseline": cpu,
             "wall_s": round(wall_max, 4),
@@ -216,6 +216,28 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     ver.close()
+
+
+def host_path(ver, batch, R, strict, reps=3):
+    """PCIe-inclusive rate of mochi_verify_batch (host buffers in, verdicts out):
+    the chunked upload/compute/download pipeline timed by its own stream events
+    (first H2D start -> last D2H end), best of `reps`, for pinned in-place arrays
+    (mochi_host_alloc, the intended drop-in layout) and for pageable arrays
+    (staged through pinned buffers; `wall` also counts that host memcpy)."""
+    N = batch.n_grants
+    out = {}
+    pinned = batch.pinned()
+    for name, b in (("pinned", pinned), ("pageable", batch)):
+        best_dev, best_wall = float("inf"), float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            v = ver.verify(b, R, strict)
+            best_wall = min(best_wall, time.perf_counter() - t0)
+            best_dev = min(best_dev, v.timing_ms["total"] / 1e3)
+        out[f"{name}_grants_per_s"] = round(N / best_dev, 1)
+        out[f"{name}_wall_grants_per_s"] = round(N / best_wall, 1)
+    out["note"] = "chunked pipeline, 262144-grant chunks; device-event span unless *_wall_*"
+    return out
 
 
 def run_cpu_baseline(args, R, k, flags_out):

@@ -152,10 +152,12 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
 void mochi_ctx_destroy(mochi_ctx* ctx);
 
 /*
- * Verify a batch held in HOST memory: stages it through pinned buffers with
- * hipMemcpyAsync on the context's stream, runs grant prep + RSA verify +
- * certificate tally, copies the verdicts back.  Synchronous.  Thread-safe
- * per context (calls on one context serialize).
+ * Verify a batch held in HOST memory.  The batch is cut into chunks of whole
+ * certificates (~256k grants, env MOCHI_CHUNK_GRANTS); chunk j+1's upload
+ * (hipMemcpyAsync on a copy stream; pageable arrays staged through pinned
+ * buffers, pinned ones DMA'd in place) overlaps chunk j's kernels (grant prep
+ * + RSA verify + certificate tally) and chunk j-1's verdict download.
+ * Synchronous.  Thread-safe per context (calls on one context serialize).
  */
 int mochi_verify_batch(mochi_ctx* ctx, const mochi_batch* batch, const mochi_params* params,
                        mochi_verdicts* out);
@@ -190,9 +192,26 @@ int mochi_rsa_public_op(mochi_ctx* ctx, uint32_t n, const uint8_t* sig_be, const
 int mochi_ctx_set_profiling(mochi_ctx* ctx, int on);
 int mochi_ctx_read_profile(mochi_ctx* ctx, float* stage_ms, uint32_t n_stages, uint32_t* n_calls);
 
-/* Stream-event timings of the last mochi_verify_batch() call on this context:
- * host->device copy, kernels, device->host copy (milliseconds). */
+/* Stream-event timings of the last mochi_verify_batch() call on this context
+ * (milliseconds).  The host path is a chunked pipeline (uploads, kernels and
+ * downloads of consecutive chunks overlap), so: h2d_ms = the first chunk's
+ * upload (nothing else runs yet), kernels_ms = first kernel start -> last
+ * kernel end, d2h_ms = the last chunk's download; mochi_ctx_last_total_ms
+ * gives first upload start -> last download end. */
 int mochi_ctx_last_timing(mochi_ctx* ctx, float* h2d_ms, float* kernels_ms, float* d2h_ms);
+int mochi_ctx_last_total_ms(mochi_ctx* ctx, float* total_ms);
+
+/* Host-path chunk size target in grants (0 = default: env MOCHI_CHUNK_GRANTS
+ * or 262144).  Chunks always hold whole certificates, 32 at a time. */
+int mochi_ctx_set_chunk_grants(mochi_ctx* ctx, uint32_t grants);
+
+/*
+ * Pinned (page-locked) host memory for building batches in place: arrays of a
+ * mochi_batch that live in such memory are DMA'd straight to the device by
+ * mochi_verify_batch (no staging copy).  NULL on failure.
+ */
+void* mochi_host_alloc(uint64_t bytes);
+void mochi_host_free(void* ptr);
 
 /*
  * Producer side (the Write1 signing site the reference leaves as a TODO:

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,12 @@ int fail(int code, const char* fmt, ...) {
   va_end(ap);
   g_err = buf;
   return code;
+}
+
+uint32_t default_chunk_grants() {
+  const char* e = getenv("MOCHI_CHUNK_GRANTS");
+  const long x = e ? atol(e) : 0;
+  return (uint32_t)(x > 0 ? x : 262144);
 }
 
 #define HIP_TRY(expr)                                                                        \
@@ -158,8 +165,12 @@ struct mochi_ctx {
   // host-path device copies
   DevBuf dev_in, dev_out;
   PinnedBuf pin_in, pin_out;
+  hipStream_t s_in = nullptr, s_out = nullptr;  // host-path copy streams
+  std::vector<hipEvent_t> chunk_ev;              // host-path chunk hand-offs
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  float last_ms[3] = {0, 0, 0};  // h2d, kernels, d2h of the last host-path call
+  float last_ms[3] = {0, 0, 0};  // first upload, compute span, last download of the last host-path call
+  float last_total_ms = 0;       // whole pipelined host-path call (first H2D start -> last D2H end)
+  uint32_t chunk_grants = 0;     // host-path chunk target (grants), mochi_ctx_set_chunk_grants
   // per-stage profiling (mochi_ctx_set_profiling): one event set per verify call
   bool profiling = false;
   std::vector<std::vector<hipEvent_t>> prof_sets;
@@ -211,9 +222,12 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
   mochi_ctx* c = new mochi_ctx;
   c->device = device;
   c->n_keys = n_keys;
+  c->chunk_grants = default_chunk_grants();
   int save = 0;
   (void)hipGetDevice(&save);
   bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_keys, sizeof(mochi::KeyEntry) * n_keys) == hipSuccess &&
             hipMemcpy(c->d_keys, table.data(), sizeof(mochi::KeyEntry) * n_keys, hipMemcpyHostToDevice) == hipSuccess;
   for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
@@ -232,8 +246,12 @@ void mochi_ctx_destroy(mochi_ctx* c) {
   (void)hipGetDevice(&save);
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->s_out) (void)hipStreamSynchronize(c->s_out);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->chunk_ev) (void)hipEventDestroy(e);
+  if (c->s_in) (void)hipStreamDestroy(c->s_in);
+  if (c->s_out) (void)hipStreamDestroy(c->s_out);
   if (c->d_keys) (void)hipFree(c->d_keys);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -335,6 +353,238 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   return MOCHI_OK;
 }
 
+// ---- host path: chunked H2D / compute / D2H pipeline ------------------------
+//
+// The batch is cut at certificate boundaries (multiples of 32 certificates, so
+// every chunk's accept bits start on a word) into chunks of ~kChunkGrants
+// grants.  Chunk j's inputs go up on the copy-in stream, its kernels run on the
+// context stream once they have landed, and its verdicts come down on the
+// copy-out stream while chunk j+1 computes.  Every chunk has its own input
+// region on the device and writes disjoint output slices, so the only
+// cross-stream ordering is one event per hand-off.  Sources that are already
+// pinned (mochi_host_alloc) are DMA'd in place; others are staged through the
+// context's pinned buffer with a parallel memcpy.
+bool is_pinned(const void* ptr) {
+  if (!ptr) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+void par_memcpy(void* dst, const void* src, size_t n) {
+  constexpr size_t kPar = 8u << 20;
+  if (n < kPar) {
+    memcpy(dst, src, n);
+    return;
+  }
+  const unsigned hw = std::thread::hardware_concurrency();
+  const unsigned nt = hw < 2 ? 1 : hw > 8 ? 8 : hw;
+  const size_t per = (n + nt - 1) / nt;
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; t++) {
+    const size_t lo = t * per;
+    if (lo >= n) break;
+    const size_t len = per < n - lo ? per : n - lo;
+    th.emplace_back([=] { memcpy((char*)dst + lo, (const char*)src + lo, len); });
+  }
+  memcpy(dst, src, per < n ? per : n);
+  for (auto& x : th) x.join();
+}
+
+int ensure_scratch(mochi_ctx* c, uint32_t N) {
+  const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
+  int rc;
+  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) ||
+      (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
+      (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
+      (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
+      (rc = c->total.ensure(sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
+      (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots)))
+    return rc;
+  return MOCHI_OK;
+}
+
+int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o) {
+  const uint32_t N = b->n_grants, C = b->n_certs;
+  // --- plan chunks ---
+  struct Chunk {
+    uint32_t c0, c1, g0, g1, o0, o1;
+    uint64_t lo, hi;  // grant byte range [lo, hi) in grant_bytes
+    size_t seg[11];   // device/staging offsets of the 11 input segments
+  };
+  std::vector<Chunk> ch;
+  uint32_t max_grants = 0;
+  for (uint32_t c0 = 0; c0 < C || (C == 0 && ch.empty());) {
+    uint32_t c1 = c0;
+    do c1 = c1 + 32 < C ? c1 + 32 : C;
+    while (c1 < C && b->cert_grant_off[c1] - b->cert_grant_off[c0] < c->chunk_grants);
+    Chunk k{};
+    k.c0 = c0;
+    k.c1 = c1;
+    k.g0 = b->cert_grant_off[c0];
+    k.g1 = b->cert_grant_off[c1];
+    k.o0 = b->cert_op_off[c0];
+    k.o1 = b->cert_op_off[c1];
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t g = k.g0; g < k.g1; g++) {
+      lo = b->grant_off[g] < lo ? b->grant_off[g] : lo;
+      const uint64_t e = b->grant_off[g] + b->grant_len[g];
+      hi = e > hi ? e : hi;
+    }
+    k.lo = k.g1 > k.g0 ? lo : 0;
+    k.hi = k.g1 > k.g0 ? hi : 0;
+    if (k.g1 - k.g0 > max_grants) max_grants = k.g1 - k.g0;
+    ch.push_back(k);
+    if (C == 0) break;
+    c0 = c1;
+  }
+  const size_t nchunks = ch.size();
+  // --- input layout: per chunk, 11 segments (same order as mochi_batch) ---
+  auto seg_bytes = [&](const Chunk& k, int i) -> size_t {
+    const size_t ng = k.g1 - k.g0, nc = k.c1 - k.c0, no = k.o1 - k.o0;
+    switch (i) {
+      case 0: return (size_t)(k.hi - k.lo);
+      case 1: return sizeof(uint64_t) * ng;
+      case 2: return sizeof(uint32_t) * ng;
+      case 3: return (size_t)MOCHI_RSA_BYTES * ng;
+      case 4: return sizeof(uint16_t) * ng;
+      case 5: return ng;
+      case 6: case 7: return sizeof(uint32_t) * (nc + 1);
+      case 8: case 9: return no;
+      default: return (size_t)MOCHI_TXN_HASH_BYTES * nc;
+    }
+  };
+  auto seg_src = [&](const Chunk& k, int i) -> const void* {
+    switch (i) {
+      case 0: return b->grant_bytes + k.lo;
+      case 1: return b->grant_off + k.g0;
+      case 2: return b->grant_len + k.g0;
+      case 3: return b->sig + (size_t)MOCHI_RSA_BYTES * k.g0;
+      case 4: return b->signer + k.g0;
+      case 5: return b->grant_key + k.g0;
+      case 6: case 7: return nullptr;  // rebased CSR, always staged
+      case 8: return b->op_key + k.o0;
+      case 9: return b->op_flags + k.o0;
+      default: return b->expected_hash + (size_t)MOCHI_TXN_HASH_BYTES * k.c0;
+    }
+  };
+  size_t in_total = 0;
+  for (auto& k : ch)
+    for (int i = 0; i < 11; i++) {
+      k.seg[i] = in_total;
+      in_total = align_up(in_total + seg_bytes(k, i), 256);
+    }
+  // --- output layout: whole-batch slices ---
+  const size_t nbits_g = ((size_t)N + 31) / 32 * 4, nbits_c = ((size_t)C + 31) / 32 * 4;
+  size_t out_total = 0;
+  auto take = [&](size_t bytes) {
+    const size_t off = out_total;
+    out_total = align_up(out_total + bytes, 256);
+    return off;
+  };
+  const size_t o_flags = take(N), o_ts = take(o->grant_ts ? sizeof(int64_t) * N : 0), o_acc = take(nbits_c),
+               o_reason = take(o->cert_reason ? C : 0), o_fail = take(o->cert_fail_op ? C : 0),
+               o_gbits = take(o->grant_valid_bits ? nbits_g : 0);
+  int rc;
+  if ((rc = c->pin_in.ensure(in_total)) || (rc = c->dev_in.ensure(in_total)) || (rc = c->pin_out.ensure(out_total)) ||
+      (rc = c->dev_out.ensure(out_total)) || (rc = ensure_scratch(c, max_grants)))
+    return rc;
+  while (c->chunk_ev.size() < 2 * nchunks) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->chunk_ev.push_back(e);
+  }
+  bool pinned[11];
+  for (int i = 0; i < 11; i++) pinned[i] = i != 6 && i != 7 && is_pinned(seg_src(ch[0], i));
+  uint8_t* pin = (uint8_t*)c->pin_in.p;
+  uint8_t* din = c->dev_in.as<uint8_t>();
+  uint8_t* dout = c->dev_out.as<uint8_t>();
+  uint8_t* pout = (uint8_t*)c->pin_out.p;
+  hipStream_t st = c->stream;
+  HIP_TRY(hipEventRecord(c->ev[0], c->s_in));
+  for (size_t j = 0; j < nchunks; j++) {
+    Chunk& k = ch[j];
+    // stage + upload
+    uint32_t* cg = (uint32_t*)(pin + k.seg[6]);
+    uint32_t* co = (uint32_t*)(pin + k.seg[7]);
+    for (uint32_t x = k.c0; x <= k.c1; x++) {
+      cg[x - k.c0] = b->cert_grant_off[x] - k.g0;
+      co[x - k.c0] = b->cert_op_off[x] - k.o0;
+    }
+    for (int i = 0; i < 11; i++) {
+      const size_t n = seg_bytes(k, i);
+      if (!n) continue;
+      const void* src = pin + k.seg[i];
+      if (pinned[i]) src = seg_src(k, i);
+      else if (i != 6 && i != 7) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
+      HIP_TRY(hipMemcpyAsync(din + k.seg[i], src, n, hipMemcpyHostToDevice, c->s_in));
+    }
+    HIP_TRY(hipEventRecord(c->chunk_ev[2 * j], c->s_in));
+    // compute
+    HIP_TRY(hipStreamWaitEvent(st, c->chunk_ev[2 * j], 0));
+    if (j == 0) HIP_TRY(hipEventRecord(c->ev[1], st));
+    mochi_batch db;
+    memset(&db, 0, sizeof db);
+    db.n_grants = k.g1 - k.g0;
+    db.n_certs = k.c1 - k.c0;
+    db.n_ops = k.o1 - k.o0;
+    db.grant_bytes_len = k.hi - k.lo;
+    db.grant_bytes = din + k.seg[0] - k.lo;  // kernels add the absolute grant_off
+    db.grant_off = (const uint64_t*)(din + k.seg[1]);
+    db.grant_len = (const uint32_t*)(din + k.seg[2]);
+    db.sig = din + k.seg[3];
+    db.signer = (const uint16_t*)(din + k.seg[4]);
+    db.grant_key = din + k.seg[5];
+    db.cert_grant_off = (const uint32_t*)(din + k.seg[6]);
+    db.cert_op_off = (const uint32_t*)(din + k.seg[7]);
+    db.op_key = din + k.seg[8];
+    db.op_flags = din + k.seg[9];
+    db.expected_hash = din + k.seg[10];
+    mochi_verdicts dv;
+    memset(&dv, 0, sizeof dv);
+    dv.grant_flags = dout + o_flags + k.g0;
+    dv.grant_ts = o->grant_ts ? (int64_t*)(dout + o_ts) + k.g0 : nullptr;
+    dv.cert_accept_bits = (uint32_t*)(dout + o_acc) + k.c0 / 32;
+    dv.cert_reason = o->cert_reason ? dout + o_reason + k.c0 : nullptr;
+    dv.cert_fail_op = o->cert_fail_op ? dout + o_fail + k.c0 : nullptr;
+    if ((rc = run_device(c, &db, p, &dv, st))) return rc;
+    if (j + 1 == nchunks && o->grant_valid_bits && N)
+      HIP_TRY(mochi::launch_pack_bits(dout + o_flags, N, MOCHI_GRANT_SIG_OK, (uint32_t*)(dout + o_gbits), st));
+    if (j + 1 == nchunks) HIP_TRY(hipEventRecord(c->ev[2], st));
+    HIP_TRY(hipEventRecord(c->chunk_ev[2 * j + 1], st));
+    // download this chunk's verdict slices
+    HIP_TRY(hipStreamWaitEvent(c->s_out, c->chunk_ev[2 * j + 1], 0));
+    auto down = [&](size_t off, size_t bytes) -> hipError_t {
+      return bytes ? hipMemcpyAsync(pout + off, dout + off, bytes, hipMemcpyDeviceToHost, c->s_out) : hipSuccess;
+    };
+    const size_t ng = k.g1 - k.g0, nc = k.c1 - k.c0;
+    const size_t acc_words = j + 1 == nchunks ? nbits_c / 4 - k.c0 / 32 : nc / 32;
+    if (o->grant_flags) HIP_TRY(down(o_flags + k.g0, ng));
+    if (o->grant_ts) HIP_TRY(down(o_ts + sizeof(int64_t) * k.g0, sizeof(int64_t) * ng));
+    HIP_TRY(down(o_acc + 4 * (size_t)(k.c0 / 32), 4 * acc_words));
+    if (o->cert_reason) HIP_TRY(down(o_reason + k.c0, nc));
+    if (o->cert_fail_op) HIP_TRY(down(o_fail + k.c0, nc));
+    if (j + 1 == nchunks && o->grant_valid_bits) HIP_TRY(down(o_gbits, nbits_g));
+  }
+  HIP_TRY(hipEventRecord(c->ev[3], c->s_out));
+  if (hipStreamSynchronize(c->s_out) != hipSuccess)
+    return fail(MOCHI_EHIP, "stream sync failed: %s", hipGetErrorString(hipGetLastError()));
+  (void)hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[1]);  // first upload (not overlapped)
+  (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);  // compute span
+  (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);  // last download (not overlapped)
+  (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
+  void* dsts[] = {o->grant_flags, o->grant_ts, o->cert_accept_bits, o->cert_reason, o->cert_fail_op,
+                  o->grant_valid_bits};
+  const size_t offs[] = {o_flags, o_ts, o_acc, o_reason, o_fail, o_gbits};
+  const size_t lens[] = {(size_t)N, sizeof(int64_t) * N, nbits_c, (size_t)C, (size_t)C, nbits_g};
+  for (int i = 0; i < 6; i++)
+    if (dsts[i] && lens[i]) memcpy(dsts[i], pout + offs[i], lens[i]);
+  return MOCHI_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -360,103 +610,34 @@ int mochi_verify_batch(mochi_ctx* c, const mochi_batch* b, const mochi_params* p
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
-  const uint32_t N = b->n_grants, C = b->n_certs, O = b->n_ops;
-  // --- stage inputs: one pinned region, one H2D copy ---
-  struct Seg {
-    const void* src;
-    size_t bytes;
-    size_t off;
-  };
-  Seg in[] = {
-      {b->grant_bytes, (size_t)b->grant_bytes_len, 0},
-      {b->grant_off, sizeof(uint64_t) * N, 0},
-      {b->grant_len, sizeof(uint32_t) * N, 0},
-      {b->sig, (size_t)MOCHI_RSA_BYTES * N, 0},
-      {b->signer, sizeof(uint16_t) * N, 0},
-      {b->grant_key, (size_t)N, 0},
-      {b->cert_grant_off, sizeof(uint32_t) * (C + 1), 0},
-      {b->cert_op_off, sizeof(uint32_t) * (C + 1), 0},
-      {b->op_key, (size_t)O, 0},
-      {b->op_flags, (size_t)O, 0},
-      {b->expected_hash, (size_t)MOCHI_TXN_HASH_BYTES * C, 0},
-  };
-  size_t in_total = 0;
-  for (auto& s : in) {
-    s.off = in_total;
-    in_total = align_up(in_total + s.bytes, 256);
-  }
-  const size_t nbits_g = ((size_t)N + 31) / 32 * 4, nbits_c = ((size_t)C + 31) / 32 * 4;
-  Seg outs[] = {{o->grant_valid_bits, o->grant_valid_bits ? nbits_g : 0, 0},
-                {o->grant_flags, o->grant_flags ? (size_t)N : 0, 0},
-                {o->grant_ts, o->grant_ts ? sizeof(int64_t) * N : 0, 0},
-                {o->cert_accept_bits, nbits_c, 0},
-                {o->cert_reason, o->cert_reason ? (size_t)C : 0, 0},
-                {o->cert_fail_op, o->cert_fail_op ? (size_t)C : 0, 0}};
-  size_t out_total = 0;
-  for (auto& s : outs) {
-    s.off = out_total;
-    out_total = align_up(out_total + s.bytes, 256);
-  }
-  if ((rc = c->pin_in.ensure(in_total)) || (rc = c->dev_in.ensure(in_total)) || (rc = c->pin_out.ensure(out_total)) ||
-      (rc = c->dev_out.ensure(out_total))) {
-    (void)hipSetDevice(save);
-    return rc;
-  }
-  uint8_t* pin = (uint8_t*)c->pin_in.p;
-  for (auto& s : in)
-    if (s.bytes) memcpy(pin + s.off, s.src, s.bytes);
-  uint8_t* din = c->dev_in.as<uint8_t>();
-  uint8_t* dout = c->dev_out.as<uint8_t>();
-  hipStream_t st = c->stream;
-  (void)hipEventRecord(c->ev[0], st);
-  if (hipMemcpyAsync(din, pin, in_total, hipMemcpyHostToDevice, st) != hipSuccess) {
-    (void)hipSetDevice(save);
-    return fail(MOCHI_EHIP, "H2D copy failed");
-  }
-  (void)hipEventRecord(c->ev[1], st);
-  mochi_batch db = *b;
-  db.grant_bytes = din + in[0].off;
-  db.grant_off = (const uint64_t*)(din + in[1].off);
-  db.grant_len = (const uint32_t*)(din + in[2].off);
-  db.sig = din + in[3].off;
-  db.signer = (const uint16_t*)(din + in[4].off);
-  db.grant_key = din + in[5].off;
-  db.cert_grant_off = (const uint32_t*)(din + in[6].off);
-  db.cert_op_off = (const uint32_t*)(din + in[7].off);
-  db.op_key = din + in[8].off;
-  db.op_flags = din + in[9].off;
-  db.expected_hash = din + in[10].off;
-  mochi_verdicts dv;
-  dv.grant_valid_bits = o->grant_valid_bits ? (uint32_t*)(dout + outs[0].off) : nullptr;
-  dv.grant_flags = o->grant_flags ? dout + outs[1].off : nullptr;
-  dv.grant_ts = o->grant_ts ? (int64_t*)(dout + outs[2].off) : nullptr;
-  dv.cert_accept_bits = (uint32_t*)(dout + outs[3].off);
-  dv.cert_reason = o->cert_reason ? dout + outs[4].off : nullptr;
-  dv.cert_fail_op = o->cert_fail_op ? dout + outs[5].off : nullptr;
-  rc = run_device(c, &db, p, &dv, st);
-  if (rc) {
-    (void)hipSetDevice(save);
-    return rc;
-  }
-  (void)hipEventRecord(c->ev[2], st);
-  if (hipMemcpyAsync(c->pin_out.p, dout, out_total, hipMemcpyDeviceToHost, st) != hipSuccess) {
-    (void)hipSetDevice(save);
-    return fail(MOCHI_EHIP, "D2H copy failed");
-  }
-  (void)hipEventRecord(c->ev[3], st);
-  if (hipStreamSynchronize(st) != hipSuccess) {
-    (void)hipSetDevice(save);
-    return fail(MOCHI_EHIP, "stream sync failed: %s", hipGetErrorString(hipGetLastError()));
-  }
-  (void)hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[1]);
-  (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);
-  (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);
-  const uint8_t* pout = (const uint8_t*)c->pin_out.p;
-  void* dsts[] = {o->grant_valid_bits, o->grant_flags, o->grant_ts, o->cert_accept_bits, o->cert_reason,
-                  o->cert_fail_op};
-  for (int i = 0; i < 6; i++)
-    if (outs[i].bytes) memcpy(dsts[i], pout + outs[i].off, outs[i].bytes);
+  rc = run_host_pipeline(c, b, p, o);
   (void)hipSetDevice(save);
+  return rc;
+}
+
+void* mochi_host_alloc(uint64_t bytes) {
+  void* ptr = nullptr;
+  if (hipHostMalloc(&ptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    fail(MOCHI_ENOMEM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
+    return nullptr;
+  }
+  return ptr;
+}
+
+void mochi_host_free(void* ptr) {
+  if (ptr) (void)hipHostFree(ptr);
+}
+
+int mochi_ctx_set_chunk_grants(mochi_ctx* c, uint32_t grants) {
+  if (!c) return fail(MOCHI_EINVAL, "null context");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->chunk_grants = grants ? grants : default_chunk_grants();
+  return MOCHI_OK;
+}
+
+int mochi_ctx_last_total_ms(mochi_ctx* c, float* total_ms) {
+  if (!c || !total_ms) return fail(MOCHI_EINVAL, "null argument");
+  *total_ms = c->last_total_ms;
   return MOCHI_OK;
 }
 

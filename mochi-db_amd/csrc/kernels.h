@@ -56,6 +56,7 @@ inline uint64_t slot_capacity(uint32_t n_grants, uint32_t n_keys) {
 }
 
 hipError_t launch_verify(const LaunchArgs& a, hipStream_t stream);
+hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t stream);
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream);
 void launch_rsa_final(const LaunchArgs& a, hipStream_t stream);
 void launch_rsa_raw(const LaunchArgs& a, hipStream_t stream);  // dbg_y path (mochi_rsa_public_op)

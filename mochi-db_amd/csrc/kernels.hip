@@ -482,6 +482,11 @@ __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t* __restrict__ f
 // ---------------------------------------------------------------------------
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 
+hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_pack_bits, dim3(cdiv(n, 256)), dim3(256), 0, st, flags, n, mask, bits);
+  return hipGetLastError();
+}
+
 hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   const uint32_t N = a.n_grants, C = a.n_certs;
   auto mark = [&](int i) {

@@ -139,6 +139,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_ctx_read_profile.argtypes = [vp, vp, u32, vp]
     lib.mochi_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
     lib.mochi_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mochi_ctx_last_total_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    lib.mochi_ctx_set_chunk_grants.argtypes = [vp, u32]
+    lib.mochi_host_alloc.restype = vp
+    lib.mochi_host_alloc.argtypes = [ctypes.c_uint64]
+    lib.mochi_host_free.argtypes = [vp]
     if lib.mochi_abi_version() != 1:
         raise MochiError("libmochi_hip ABI mismatch")
     _lib = lib
@@ -200,6 +205,27 @@ class Batch:
             expected_hash=np.ascontiguousarray(self.expected_hash, dtype=np.uint8).reshape(-1, TXN_HASH_BYTES),
         )
 
+    def pinned(self) -> "Batch":
+        """A copy whose arrays live in one pinned host allocation (mochi_host_alloc):
+        mochi_verify_batch DMAs such arrays in place instead of staging them."""
+        b = self.normalized()
+        names = ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off",
+                 "cert_op_off", "op_key", "op_flags", "expected_hash")
+        arrs = [getattr(b, nm) for nm in names]
+        offs, total = [], 0
+        for a in arrs:
+            offs.append(total)
+            total = (total + a.nbytes + 255) // 256 * 256
+        buf = PinnedHost(total)
+        out = {}
+        for nm, a, o in zip(names, arrs, offs):
+            v = np.frombuffer(buf.view()[o:o + a.nbytes], dtype=a.dtype).reshape(a.shape)
+            v[...] = a
+            out[nm] = v
+        pb = Batch(**out)
+        pb._pinned = buf  # keep the allocation alive with the views
+        return pb
+
     def to_c(self) -> Batch_C:
         b = Batch_C()
         b.n_grants, b.n_certs, b.n_ops = self.n_grants, self.n_certs, self.n_ops
@@ -216,6 +242,25 @@ class Batch:
         b.op_flags = _ptr(self.op_flags)
         b.expected_hash = _ptr(self.expected_hash)
         return b
+
+
+class PinnedHost:
+    """Pinned host allocation from libmochi_hip (mochi_host_alloc / mochi_host_free)."""
+
+    def __init__(self, nbytes: int):
+        self.lib = load_library()
+        self.nbytes = max(int(nbytes), 1)
+        self.ptr = self.lib.mochi_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MochiError(f"mochi_host_alloc: {_err(self.lib)}")
+
+    def view(self) -> np.ndarray:
+        return np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def __del__(self):  # pragma: no cover
+        if getattr(self, "ptr", None):
+            self.lib.mochi_host_free(self.ptr)
+            self.ptr = None
 
 
 @dataclass
@@ -291,6 +336,11 @@ class Verifier:
             raise MochiError(f"mochi_ctx_create failed: {_err(self.lib)}")
         self.device = device
 
+    def set_chunk_grants(self, grants: int) -> None:
+        """Host-path pipeline chunk target (grants); 0 restores the default."""
+        if self.lib.mochi_ctx_set_chunk_grants(self.ctx, int(grants)) != OK:
+            raise MochiError(_err(self.lib))
+
     def close(self) -> None:
         if getattr(self, "ctx", None):
             self.lib.mochi_ctx_destroy(self.ctx)
@@ -311,9 +361,10 @@ class Verifier:
         rc = self.lib.mochi_verify_batch(self.ctx, ctypes.byref(bc), ctypes.byref(p), ctypes.byref(vc))
         if rc != OK:
             raise MochiError(f"mochi_verify_batch rc={rc}: {_err(self.lib)}")
-        h, k, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        h, k, d, t = ctypes.c_float(), ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
         self.lib.mochi_ctx_last_timing(self.ctx, ctypes.byref(h), ctypes.byref(k), ctypes.byref(d))
-        out.timing_ms = {"h2d": h.value, "kernels": k.value, "d2h": d.value}
+        self.lib.mochi_ctx_last_total_ms(self.ctx, ctypes.byref(t))
+        out.timing_ms = {"h2d": h.value, "kernels": k.value, "d2h": d.value, "total": t.value}
         return out
 
     STAGES = ("prep_sha256", "bucket", "rsa_pow", "rsa_final", "tally")
@@ -382,6 +433,27 @@ class DeviceBatch:
         self.op_key = t(b.op_key)
         self.op_flags = t(b.op_flags)
         self.expected_hash = t(b.expected_hash)
+
+    def pinned(self) -> "Batch":
+        """A copy whose arrays live in one pinned host allocation (mochi_host_alloc):
+        mochi_verify_batch DMAs such arrays in place instead of staging them."""
+        b = self.normalized()
+        names = ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off",
+                 "cert_op_off", "op_key", "op_flags", "expected_hash")
+        arrs = [getattr(b, nm) for nm in names]
+        offs, total = [], 0
+        for a in arrs:
+            offs.append(total)
+            total = (total + a.nbytes + 255) // 256 * 256
+        buf = PinnedHost(total)
+        out = {}
+        for nm, a, o in zip(names, arrs, offs):
+            v = np.frombuffer(buf.view()[o:o + a.nbytes], dtype=a.dtype).reshape(a.shape)
+            v[...] = a
+            out[nm] = v
+        pb = Batch(**out)
+        pb._pinned = buf  # keep the allocation alive with the views
+        return pb
 
     def to_c(self) -> Batch_C:
         b = Batch_C()

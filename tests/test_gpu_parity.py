@@ -275,3 +275,37 @@ def test_repeatable(pool4, ver4):
     a = ver4.verify(s.batch, 4, True)
     b = ver4.verify(s.batch, 4, True)
     assert_same(a, b, "repeat")
+
+
+def _scatter_blob(b: mh.Batch, seed: int) -> mh.Batch:
+    """Same grants, bytes laid out in a random order with gaps (wire-slice layout)."""
+    rng = np.random.default_rng(seed)
+    order = rng.permutation(b.n_grants)
+    blob, offs = bytearray(b"\x07" * 5), np.zeros(b.n_grants, np.uint64)
+    for i in order:
+        blob += b"\x00" * int(rng.integers(0, 4))
+        offs[i] = len(blob)
+        o, n = int(b.grant_off[i]), int(b.grant_len[i])
+        blob += b.grant_bytes[o:o + n].tobytes()
+    return mh.Batch(grant_bytes=np.frombuffer(bytes(blob), np.uint8).copy(), grant_off=offs, grant_len=b.grant_len,
+                    sig=b.sig, signer=b.signer, grant_key=b.grant_key, cert_grant_off=b.cert_grant_off,
+                    cert_op_off=b.cert_op_off, op_key=b.op_key, op_flags=b.op_flags, expected_hash=b.expected_hash)
+
+
+@pytest.mark.parametrize("chunk", [1, 1000, 50_000])
+def test_host_pipeline_chunking(pool4, chunk):
+    """mochi_verify_batch's chunked H2D/compute/D2H pipeline: chunk sizes from 32
+    certificates up, a certificate count that is not a multiple of 32, pinned
+    in-place arrays and a scattered grant blob all give the oracle's verdicts."""
+    ver = mh.Verifier(pool4.moduli, 0)
+    ver.set_chunk_grants(chunk)
+    s = W.make_batch(pool4, 2501, first_cert=123)
+    o = O.verify_batch(pool4.moduli, s.batch, 4, True, 8)
+    g = ver.verify(s.batch, 4, True)
+    assert_same(g, o, f"chunk={chunk}")
+    assert g.timing_ms["total"] > 0
+    gp = ver.verify(s.batch.pinned(), 4, True)
+    assert_same(gp, o, f"pinned chunk={chunk}")
+    gs = ver.verify(_scatter_blob(s.batch, chunk), 4, True)
+    assert_same(gs, o, f"scattered chunk={chunk}")
+    ver.close()
