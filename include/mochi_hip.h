@@ -70,6 +70,10 @@ enum mochi_reason {
   /* a grant's bytes are not a parseable proto3 Grant (the reference would fail
    * in the Netty protobuf decoder, MochiServerInitializer.java:30-34). */
   MOCHI_REJECT_MALFORMED = 6,
+  /* Write2 wire path only: the message is legal protobuf but outside the
+   * device decoder's fast path (enum mochi_msg_status MOCHI_MSG_FALLBACK /
+   * MOCHI_MSG_OPS_MISMATCH); not accepted here, verify it on the host path. */
+  MOCHI_UNDECIDED = 7,
 };
 
 /* op_flags bits (one byte per transaction operation). */
@@ -276,6 +280,89 @@ enum mochi_write1_decision {
 int mochi_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const uint8_t* resp_kind,
                           const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
                           const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision);
+
+/* ------------------------------------------------------------------------
+ * Write2ToServer wire path: the device decodes the received protobuf bytes.
+ *
+ * Replaces the SoA assembly a caller of mochi_verify_batch has to do: it takes
+ * the Write2ToServer message bodies exactly as they arrived
+ * (MochiProtocol.proto:144-147, field 110 of a
+ * ProtocolMessage), decodes them on the device with protobuf-java 3.16.3
+ * semantics (map fields keep first-insertion order with last-value-wins,
+ * unknown fields skipped, proto3 strings UTF-8 checked, any malformation fails
+ * the whole message) and verifies them.  Grant bytes are verified in place
+ * (zero copy); each grant's signature is MultiGrant.grantSignatures[objectId]
+ * (the field INTEGRATION.md adds as MochiProtocol.proto:123's TODO) and its
+ * signer is the key whose server id (mochi_ctx_set_server_ids) equals
+ * MultiGrant.serverId.
+ * ------------------------------------------------------------------------ */
+
+/* Per-message decode status. */
+enum mochi_msg_status {
+  MOCHI_MSG_OK = 0,
+  /* not a parseable Write2ToServer: protobuf-java's parser would throw
+   * InvalidProtocolBufferException in the Netty decoder
+   * (MochiServerInitializer.java:30-34) -> reason MOCHI_REJECT_MALFORMED */
+  MOCHI_MSG_MALFORMED = 1,
+  /* legal, but outside the device decoder's fast path -> reason
+   * MOCHI_UNDECIDED: writeCertificate or transaction given more than once; a
+   * map entry whose MultiGrant or Grant value is given more than once; a Grant
+   * whose bytes are not the canonical encoding Grant.toByteArray() would give
+   * (MochiProtocol.java:7556-7574); more than 32 MultiGrants, 64 grants per
+   * MultiGrant or 64 operations */
+  MOCHI_MSG_FALLBACK = 2,
+  /* op_flags_off gives a different operation count than the message holds */
+  MOCHI_MSG_OPS_MISMATCH = 3,
+};
+
+typedef struct mochi_write2_batch {
+  uint32_t n_msgs; /* M */
+  uint32_t _pad0;
+  uint64_t wire_len;              /* size of wire                                             */
+  const uint8_t* wire;            /* blob holding every Write2ToServer body                    */
+  const uint64_t* msg_off;        /* [M] byte offset of message m in wire                      */
+  const uint32_t* msg_len;        /* [M] byte length of message m                              */
+  const uint32_t* op_flags_off;   /* [M+1] CSR into op_flags; NULL = every op LOCAL|HAS_SVOC    */
+  const uint8_t* op_flags;        /* MOCHI_OP_* per operation, transaction order               */
+  const uint8_t* expected_hash;   /* [M * 128] objectSHA512(transaction), lowercase hex         */
+} mochi_write2_batch;
+
+/* Server-id table of the context: key i of the key table belongs to the server
+ * whose MultiGrant.serverId is ids[id_off[i], id_off[i+1]).  n_ids must equal
+ * the context's key count; ids <= 256 bytes each. */
+int mochi_ctx_set_server_ids(mochi_ctx* ctx, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids);
+
+/* Decode + verify M Write2ToServer messages held in HOST memory.  Only the
+ * certificate-level verdict arrays of `out` are written (grant-level pointers
+ * must be NULL); msg_status[M] receives enum mochi_msg_status.  Synchronous. */
+int mochi_verify_write2(mochi_ctx* ctx, const mochi_write2_batch* batch, const mochi_params* params,
+                        mochi_verdicts* out, uint8_t* msg_status);
+
+/* Same with every pointer of `batch`, `out` and msg_status in DEVICE memory,
+ * enqueued on `stream` (hipStream_t; NULL = null stream).  The decoded batch
+ * is sized on the device; the call waits for its grant / op totals. */
+int mochi_verify_write2_device(mochi_ctx* ctx, const mochi_write2_batch* batch, const mochi_params* params,
+                               mochi_verdicts* out, uint8_t* msg_status, void* stream);
+
+/* The device decoder's output for M messages in HOST memory (inspection and
+ * tests; mochi_verify_write2 never copies it back).  Arrays are allocated by
+ * the library; release them with mochi_write2_decoded_free.  grant_off is
+ * relative to the start of `wire`. */
+typedef struct mochi_write2_decoded {
+  uint32_t n_msgs, n_grants, n_ops, _pad0;
+  uint64_t* grant_off;      /* [N] */
+  uint32_t* grant_len;      /* [N] */
+  uint8_t* sig;             /* [N * 256] */
+  uint16_t* signer;         /* [N] key index, 0xFFFF = unknown serverId */
+  uint8_t* grant_key;       /* [N] op key slot, 0xFF = no op names it */
+  uint32_t* cert_grant_off; /* [M+1] */
+  uint32_t* cert_op_off;    /* [M+1] */
+  uint8_t* op_key;          /* [O] */
+  uint8_t* op_flags;        /* [O] */
+  uint8_t* msg_status;      /* [M] enum mochi_msg_status */
+} mochi_write2_decoded;
+int mochi_write2_decode(mochi_ctx* ctx, const mochi_write2_batch* batch, mochi_write2_decoded* out);
+void mochi_write2_decoded_free(mochi_write2_decoded* d);
 
 #ifdef __cplusplus
 }

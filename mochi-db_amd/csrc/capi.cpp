@@ -171,6 +171,12 @@ struct mochi_ctx {
   float last_ms[3] = {0, 0, 0};  // first upload, compute span, last download of the last host-path call
   float last_total_ms = 0;       // whole pipelined host-path call (first H2D start -> last D2H end)
   uint32_t chunk_grants = 0;     // host-path chunk target (grants), mochi_ctx_set_chunk_grants
+  // Write2 wire path: server-id table + decode scratch
+  DevBuf ids, id_off;
+  uint32_t n_ids = 0;
+  DevBuf w2_cnt_g, w2_cnt_o, w2_status, w2_scan, w2_cg, w2_co, w2_goff, w2_glen, w2_sig, w2_signer, w2_gkey,
+      w2_okey, w2_oflags;
+  PinnedBuf w2_tot;
   // per-stage profiling (mochi_ctx_set_profiling): one event set per verify call
   bool profiling = false;
   std::vector<std::vector<hipEvent_t>> prof_sets;
@@ -585,6 +591,101 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
   return MOCHI_OK;
 }
 
+// ---- Write2ToServer wire path -------------------------------------------------
+// Decode on the device (w2_decode.hip), then the ordinary verify path over the
+// decoded batch, then the per-message status fix-up.  All pointers device.
+int run_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+                      uint8_t* status, hipStream_t st, mochi::W2Args* decoded_only = nullptr) {
+  const uint32_t M = w->n_msgs;
+  if (c->n_ids != c->n_keys) return fail(MOCHI_EINVAL, "server ids not set (mochi_ctx_set_server_ids)");
+  size_t scan_bytes = 0;
+  HIP_TRY(mochi::w2_scan_temp_bytes(M + 1, &scan_bytes));
+  int rc;
+  if ((rc = c->w2_cnt_g.ensure(4 * ((size_t)M + 1))) || (rc = c->w2_cnt_o.ensure(4 * ((size_t)M + 1))) ||
+      (rc = c->w2_scan.ensure(scan_bytes)) || (rc = c->w2_cg.ensure(4 * ((size_t)M + 1))) ||
+      (rc = c->w2_co.ensure(4 * ((size_t)M + 1))) || (rc = c->w2_tot.ensure(8)) ||
+      (!status && (rc = c->w2_status.ensure(M ? M : 1))))
+    return rc;
+  mochi::W2Args a;
+  memset(&a, 0, sizeof a);
+  a.wire = w->wire;
+  a.msg_off = w->msg_off;
+  a.msg_len = w->msg_len;
+  a.M = M;
+  a.flags_off = w->op_flags_off;
+  a.flags_in = w->op_flags;
+  a.ids = c->ids.as<uint8_t>();
+  a.id_off = c->id_off.as<uint32_t>();
+  a.n_ids = c->n_ids;
+  a.cnt_g = c->w2_cnt_g.as<uint32_t>();
+  a.cnt_o = c->w2_cnt_o.as<uint32_t>();
+  a.status = status ? status : c->w2_status.as<uint8_t>();
+  a.scan_temp = c->w2_scan.p;
+  a.scan_temp_bytes = c->w2_scan.cap;
+  a.cert_grant_off = c->w2_cg.as<uint32_t>();
+  a.cert_op_off = c->w2_co.as<uint32_t>();
+  HIP_TRY(mochi::launch_w2_count(a, st));
+  // totals decide the decoded-array sizes
+  uint32_t* tot = (uint32_t*)c->w2_tot.p;
+  HIP_TRY(hipMemcpyAsync(tot, a.cert_grant_off + M, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(tot + 1, a.cert_op_off + M, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint32_t N = tot[0], O = tot[1];
+  if ((rc = c->w2_goff.ensure(8 * (size_t)N)) || (rc = c->w2_glen.ensure(4 * (size_t)N)) ||
+      (rc = c->w2_sig.ensure((size_t)MOCHI_RSA_BYTES * N)) || (rc = c->w2_signer.ensure(2 * (size_t)N)) ||
+      (rc = c->w2_gkey.ensure(N)) || (rc = c->w2_okey.ensure(O)) || (rc = c->w2_oflags.ensure(O)))
+    return rc;
+  a.grant_off = c->w2_goff.as<uint64_t>();
+  a.grant_len = c->w2_glen.as<uint32_t>();
+  a.sig = c->w2_sig.as<uint8_t>();
+  a.signer = c->w2_signer.as<uint16_t>();
+  a.grant_key = c->w2_gkey.as<uint8_t>();
+  a.op_key = c->w2_okey.as<uint8_t>();
+  a.op_flags = c->w2_oflags.as<uint8_t>();
+  HIP_TRY(mochi::launch_w2_emit(a, st));
+  if (decoded_only) {
+    *decoded_only = a;
+    return MOCHI_OK;
+  }
+  mochi_batch db;
+  memset(&db, 0, sizeof db);
+  db.n_grants = N;
+  db.n_certs = M;
+  db.n_ops = O;
+  db.grant_bytes_len = w->wire_len;
+  db.grant_bytes = w->wire;
+  db.grant_off = a.grant_off;
+  db.grant_len = a.grant_len;
+  db.sig = a.sig;
+  db.signer = a.signer;
+  db.grant_key = a.grant_key;
+  db.cert_grant_off = a.cert_grant_off;
+  db.cert_op_off = a.cert_op_off;
+  db.op_key = a.op_key;
+  db.op_flags = a.op_flags;
+  db.expected_hash = w->expected_hash;
+  mochi_verdicts dv;
+  memset(&dv, 0, sizeof dv);
+  dv.cert_accept_bits = o->cert_accept_bits;
+  dv.cert_reason = o->cert_reason;
+  dv.cert_fail_op = o->cert_fail_op;
+  if ((rc = run_device(c, &db, p, &dv, st))) return rc;
+  HIP_TRY(mochi::launch_w2_fixup(a, o->cert_accept_bits, o->cert_reason, o->cert_fail_op, st));
+  return MOCHI_OK;
+}
+
+int check_write2_header(const mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p,
+                        const mochi_verdicts* o) {
+  if (!c || !w || !p || !o) return fail(MOCHI_EINVAL, "null argument");
+  if (o->grant_valid_bits || o->grant_flags || o->grant_ts)
+    return fail(MOCHI_EINVAL, "grant-level outputs are not produced on the Write2 wire path");
+  if (w->n_msgs && (!o->cert_accept_bits || !w->wire || !w->msg_off || !w->msg_len || !w->expected_hash))
+    return fail(MOCHI_EINVAL, "wire / msg_off / msg_len / expected_hash / cert_accept_bits required");
+  if (w->op_flags_off && !w->op_flags) return fail(MOCHI_EINVAL, "op_flags required with op_flags_off");
+  if (p->replication_factor == 0) return fail(MOCHI_EINVAL, "replication_factor must be > 0");
+  return MOCHI_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -639,6 +740,184 @@ int mochi_ctx_last_total_ms(mochi_ctx* c, float* total_ms) {
   if (!c || !total_ms) return fail(MOCHI_EINVAL, "null argument");
   *total_ms = c->last_total_ms;
   return MOCHI_OK;
+}
+
+int mochi_ctx_set_server_ids(mochi_ctx* c, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids) {
+  if (!c || !ids || !id_off) return fail(MOCHI_EINVAL, "null argument");
+  if (n_ids != c->n_keys) return fail(MOCHI_EINVAL, "n_ids (%u) must equal the key count (%u)", n_ids, c->n_keys);
+  if (id_off[0] != 0) return fail(MOCHI_EINVAL, "id_off[0] must be 0");
+  for (uint32_t i = 0; i < n_ids; i++)
+    if (id_off[i + 1] < id_off[i] || id_off[i + 1] - id_off[i] > 256)
+      return fail(MOCHI_EINVAL, "server id %u: bad length", i);
+  std::lock_guard<std::mutex> lk(c->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  const size_t nb = id_off[n_ids];
+  int rc = c->ids.ensure(nb ? nb : 1);
+  if (!rc) rc = c->id_off.ensure(4 * ((size_t)n_ids + 1));
+  if (!rc && nb && hipMemcpy(c->ids.p, ids, nb, hipMemcpyHostToDevice) != hipSuccess) rc = fail(MOCHI_EHIP, "copy ids");
+  if (!rc && hipMemcpy(c->id_off.p, id_off, 4 * ((size_t)n_ids + 1), hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(MOCHI_EHIP, "copy id_off");
+  if (!rc) c->n_ids = n_ids;
+  (void)hipSetDevice(save);
+  return rc;
+}
+
+int mochi_verify_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+                               uint8_t* msg_status, void* stream) {
+  int rc = check_write2_header(c, w, p, o);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  rc = run_write2_device(c, w, p, o, msg_status, (hipStream_t)stream);
+  (void)hipSetDevice(save);
+  return rc;
+}
+
+static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+                              uint8_t* msg_status, mochi_write2_decoded* dec);
+
+int mochi_verify_write2(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+                        uint8_t* msg_status) {
+  int rc = check_write2_header(c, w, p, o);
+  if (rc) return rc;
+  return verify_write2_host(c, w, p, o, msg_status, nullptr);
+}
+
+int mochi_write2_decode(mochi_ctx* c, const mochi_write2_batch* w, mochi_write2_decoded* out) {
+  if (!out) return fail(MOCHI_EINVAL, "null argument");
+  memset(out, 0, sizeof *out);
+  mochi_params p = {1, 1, {0, 0}};
+  mochi_verdicts o;
+  memset(&o, 0, sizeof o);
+  uint32_t dummy = 0;
+  o.cert_accept_bits = &dummy;
+  int rc = check_write2_header(c, w, &p, &o);
+  if (rc) return rc;
+  return verify_write2_host(c, w, &p, &o, nullptr, out);
+}
+
+void mochi_write2_decoded_free(mochi_write2_decoded* d) {
+  if (!d) return;
+  free(d->grant_off);
+  free(d->grant_len);
+  free(d->sig);
+  free(d->signer);
+  free(d->grant_key);
+  free(d->cert_grant_off);
+  free(d->cert_op_off);
+  free(d->op_key);
+  free(d->op_flags);
+  free(d->msg_status);
+  memset(d, 0, sizeof *d);
+}
+
+static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+                              uint8_t* msg_status, mochi_write2_decoded* dec) {
+  int rc;
+  const uint32_t M = w->n_msgs;
+  for (uint32_t m = 0; m < M; m++)
+    if (w->msg_off[m] > w->wire_len || w->msg_len[m] > w->wire_len - w->msg_off[m])
+      return fail(MOCHI_EINVAL, "message %u lies outside wire", m);
+  std::lock_guard<std::mutex> lk(c->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  const size_t O_in = w->op_flags_off ? w->op_flags_off[M] : 0;
+  struct Seg {
+    const void* src;
+    size_t bytes, off;
+  } in[] = {{w->wire, (size_t)w->wire_len, 0},
+            {w->msg_off, 8 * (size_t)M, 0},
+            {w->msg_len, 4 * (size_t)M, 0},
+            {w->op_flags_off, w->op_flags_off ? 4 * ((size_t)M + 1) : 0, 0},
+            {w->op_flags, O_in, 0},
+            {w->expected_hash, (size_t)MOCHI_TXN_HASH_BYTES * M, 0}};
+  size_t in_total = 0;
+  for (auto& sg : in) {
+    sg.off = in_total;
+    in_total = align_up(in_total + sg.bytes, 256);
+  }
+  const size_t nbits = ((size_t)M + 31) / 32 * 4;
+  const size_t o_acc = 0, o_reason = align_up(nbits, 256), o_fail = o_reason + align_up(M, 256),
+               o_status = o_fail + align_up(M, 256), out_total = o_status + align_up(M ? M : 1, 256);
+  hipStream_t st = c->stream;
+  if ((rc = c->pin_in.ensure(in_total)) || (rc = c->dev_in.ensure(in_total)) || (rc = c->pin_out.ensure(out_total)) ||
+      (rc = c->dev_out.ensure(out_total))) {
+    (void)hipSetDevice(save);
+    return rc;
+  }
+  uint8_t* pin = (uint8_t*)c->pin_in.p;
+  uint8_t* din = c->dev_in.as<uint8_t>();
+  uint8_t* dout = c->dev_out.as<uint8_t>();
+  for (auto& sg : in)
+    if (sg.bytes) par_memcpy(pin + sg.off, sg.src, sg.bytes);
+  rc = MOCHI_OK;
+  if (hipEventRecord(c->ev[0], st) != hipSuccess ||
+      hipMemcpyAsync(din, pin, in_total, hipMemcpyHostToDevice, st) != hipSuccess)
+    rc = fail(MOCHI_EHIP, "H2D copy failed");
+  mochi_write2_batch dw = *w;
+  dw.wire = din + in[0].off;
+  dw.msg_off = (const uint64_t*)(din + in[1].off);
+  dw.msg_len = (const uint32_t*)(din + in[2].off);
+  dw.op_flags_off = w->op_flags_off ? (const uint32_t*)(din + in[3].off) : nullptr;
+  dw.op_flags = w->op_flags_off ? din + in[4].off : nullptr;
+  dw.expected_hash = din + in[5].off;
+  mochi_verdicts dv;
+  memset(&dv, 0, sizeof dv);
+  dv.cert_accept_bits = (uint32_t*)(dout + o_acc);
+  dv.cert_reason = dout + o_reason;
+  dv.cert_fail_op = dout + o_fail;
+  mochi::W2Args da;
+  if (!rc) rc = run_write2_device(c, &dw, p, &dv, dout + o_status, st, dec ? &da : nullptr);
+  if (!rc && dec) {
+    // decode-only: copy the decoded SoA back (tests / inspection)
+    const uint32_t N = ((uint32_t*)c->w2_tot.p)[0], O = ((uint32_t*)c->w2_tot.p)[1];
+    dec->n_msgs = M;
+    dec->n_grants = N;
+    dec->n_ops = O;
+    dec->grant_off = (uint64_t*)malloc(8 * (size_t)N + 8);
+    dec->grant_len = (uint32_t*)malloc(4 * (size_t)N + 4);
+    dec->sig = (uint8_t*)malloc((size_t)MOCHI_RSA_BYTES * N + 1);
+    dec->signer = (uint16_t*)malloc(2 * (size_t)N + 2);
+    dec->grant_key = (uint8_t*)malloc((size_t)N + 1);
+    dec->cert_grant_off = (uint32_t*)malloc(4 * ((size_t)M + 1));
+    dec->cert_op_off = (uint32_t*)malloc(4 * ((size_t)M + 1));
+    dec->op_key = (uint8_t*)malloc((size_t)O + 1);
+    dec->op_flags = (uint8_t*)malloc((size_t)O + 1);
+    dec->msg_status = (uint8_t*)malloc((size_t)M + 1);
+    struct {
+      void* dst;
+      const void* src;
+      size_t n;
+    } cp[] = {{dec->grant_off, da.grant_off, 8 * (size_t)N},     {dec->grant_len, da.grant_len, 4 * (size_t)N},
+              {dec->sig, da.sig, (size_t)MOCHI_RSA_BYTES * N},   {dec->signer, da.signer, 2 * (size_t)N},
+              {dec->grant_key, da.grant_key, N},                 {dec->cert_grant_off, da.cert_grant_off, 4 * ((size_t)M + 1)},
+              {dec->cert_op_off, da.cert_op_off, 4 * ((size_t)M + 1)}, {dec->op_key, da.op_key, O},
+              {dec->op_flags, da.op_flags, O},                   {dec->msg_status, da.status, M}};
+    for (auto& x : cp)
+      if (!rc && x.n && hipMemcpyAsync(x.dst, x.src, x.n, hipMemcpyDeviceToHost, st) != hipSuccess)
+        rc = fail(MOCHI_EHIP, "decode copy-back failed");
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = fail(MOCHI_EHIP, "decode sync failed");
+    (void)hipSetDevice(save);
+    return rc;
+  }
+  if (!rc && (hipMemcpyAsync(c->pin_out.p, dout, out_total, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              hipEventRecord(c->ev[3], st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess))
+    rc = fail(MOCHI_EHIP, "write2 path failed: %s", hipGetErrorString(hipGetLastError()));
+  if (!rc) {
+    (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
+    const uint8_t* po = (const uint8_t*)c->pin_out.p;
+    memcpy(o->cert_accept_bits, po + o_acc, nbits);
+    if (o->cert_reason) memcpy(o->cert_reason, po + o_reason, M);
+    if (o->cert_fail_op) memcpy(o->cert_fail_op, po + o_fail, M);
+    if (msg_status) memcpy(msg_status, po + o_status, M);
+  }
+  (void)hipSetDevice(save);
+  return rc;
 }
 
 int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const uint16_t* signer, uint8_t* out_be,

@@ -55,6 +55,40 @@ inline uint64_t slot_capacity(uint32_t n_grants, uint32_t n_keys) {
   return (uint64_t)n_grants + 64ull * (n_keys < n_grants ? n_keys : n_grants);
 }
 
+// Write2ToServer wire decode (w2_decode.hip).  Device pointers.
+struct W2Args {
+  // input messages
+  const uint8_t* wire;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  uint32_t M;
+  const uint32_t* flags_off;  // [M+1] or null
+  const uint8_t* flags_in;
+  const uint8_t* ids;         // server-id table
+  const uint32_t* id_off;
+  uint32_t n_ids;
+  // scratch / outputs
+  uint32_t* cnt_g;  // [M+1]
+  uint32_t* cnt_o;  // [M+1]
+  uint8_t* status;  // [M]
+  void* scan_temp;
+  size_t scan_temp_bytes;
+  uint32_t* cert_grant_off;  // [M+1]
+  uint32_t* cert_op_off;     // [M+1]
+  uint64_t* grant_off;
+  uint32_t* grant_len;
+  uint8_t* sig;
+  uint16_t* signer;
+  uint8_t* grant_key;
+  uint8_t* op_key;
+  uint8_t* op_flags;
+};
+hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
+hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans
+hipError_t launch_w2_emit(const W2Args& a, hipStream_t stream);
+hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reason, uint8_t* fail_op,
+                           hipStream_t stream);
+
 hipError_t launch_verify(const LaunchArgs& a, hipStream_t stream);
 hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t stream);
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream);

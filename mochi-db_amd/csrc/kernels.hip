@@ -17,189 +17,9 @@
 
 #include "../../include/mochi_hip.h"
 #include "kernels.h"
-
+#include "proto_dev.h"
 
 namespace mochi {
-
-// ---------------------------------------------------------------------------
-// Byte access into the grant blob (arbitrary alignment, never reads past the
-// last byte of the grant: the blob may be a slice of a wire buffer).
-// ---------------------------------------------------------------------------
-struct ByteReader {
-  const uint8_t* base;  // grant start
-  uint32_t len;
-  uint32_t cached_idx;  // aligned word index (relative to aligned base) held in `w`
-  uint32_t w;
-  uintptr_t abase;      // base rounded down to 4
-  uint32_t shift;       // base & 3
-
-  __device__ void init(const uint8_t* p, uint32_t l) {
-    base = p;
-    len = l;
-    abase = (uintptr_t)p & ~(uintptr_t)3;
-    shift = (uint32_t)((uintptr_t)p & 3);
-    cached_idx = 0xFFFFFFFFu;
-    w = 0;
-  }
-  // byte i (i < len)
-  __device__ __forceinline__ uint32_t at(uint32_t i) {
-    const uint32_t a = i + shift;
-    const uint32_t wi = a >> 2;
-    if (wi != cached_idx) {
-      w = *(const uint32_t*)(abase + 4 * (uintptr_t)wi);  // word holds byte i: in bounds
-      cached_idx = wi;
-    }
-    return (w >> (8 * (a & 3))) & 0xFFu;
-  }
-};
-
-// ---------------------------------------------------------------------------
-// proto3 Grant parse — restates oracle_grant_parse (oracle/mochi_oracle.c),
-// which restates MochiProtocol.java:7369-7425 + protobuf-java 3.16.3
-// CodedInputStream.  Returns 1 ok / 0 malformed.
-// ---------------------------------------------------------------------------
-constexpr int kMaxGroupDepth = 16;
-
-__device__ __forceinline__ bool rd_varint(ByteReader& r, uint32_t& pos, uint64_t& v) {
-  uint64_t x = 0;
-#pragma unroll 1
-  for (int i = 0; i < 10; i++) {
-    if (pos >= r.len) return false;
-    const uint32_t c = r.at(pos++);
-    x |= (uint64_t)(c & 0x7F) << (7 * i);
-    if (!(c & 0x80)) {
-      v = x;
-      return true;
-    }
-  }
-  return false;
-}
-
-__device__ bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
-  uint32_t i = 0;
-#pragma unroll 1
-  while (i < n) {
-    const uint32_t c = r.at(off + i);
-    if (c < 0x80) {
-      // ASCII fast path: skip every remaining byte of the cached word when all
-      // of them are ASCII and inside the string (keys and the 128-char hex
-      // transactionHash are ASCII, so this is 4 bytes per step)
-      const uint32_t sub = (off + i + r.shift) & 3, rest = 4 - sub;
-      if (i + rest <= n && ((r.w >> (8 * sub)) & (0x80808080u >> (8 * sub))) == 0) i += rest;
-      else i++;
-      continue;
-    }
-    if (c < 0xC2) return false;
-    if (c < 0xE0) {
-      if (i + 1 >= n || (r.at(off + i + 1) & 0xC0) != 0x80) return false;
-      i += 2;
-      continue;
-    }
-    if (c < 0xF0) {
-      if (i + 2 >= n) return false;
-      const uint32_t c1 = r.at(off + i + 1), c2 = r.at(off + i + 2);
-      if ((c1 & 0xC0) != 0x80 || (c2 & 0xC0) != 0x80) return false;
-      if (c == 0xE0 && c1 < 0xA0) return false;
-      if (c == 0xED && c1 >= 0xA0) return false;
-      i += 3;
-      continue;
-    }
-    if (c < 0xF5) {
-      if (i + 3 >= n) return false;
-      const uint32_t c1 = r.at(off + i + 1), c2 = r.at(off + i + 2), c3 = r.at(off + i + 3);
-      if ((c1 & 0xC0) != 0x80 || (c2 & 0xC0) != 0x80 || (c3 & 0xC0) != 0x80) return false;
-      if (c == 0xF0 && c1 < 0x90) return false;
-      if (c == 0xF4 && c1 >= 0x90) return false;
-      i += 4;
-      continue;
-    }
-    return false;
-  }
-  return true;
-}
-
-__device__ __forceinline__ bool rd_string(ByteReader& r, uint32_t& pos, uint32_t& off, uint32_t& len) {
-  uint64_t l;
-  if (!rd_varint(r, pos, l)) return false;
-  const int32_t l32 = (int32_t)(uint32_t)l;
-  if (l32 < 0 || (uint32_t)l32 > r.len - pos) return false;
-  if (!valid_utf8(r, pos, (uint32_t)l32)) return false;
-  off = pos;
-  len = (uint32_t)l32;
-  pos += (uint32_t)l32;
-  return true;
-}
-
-__device__ bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
-  uint32_t pos = 0;
-  int64_t t = 0;
-  uint32_t hoff = 0, hlen = 0, ooff = 0, olen = 0;
-  uint32_t stack[kMaxGroupDepth];
-  int depth = 0;
-#pragma unroll 1
-  while (pos < r.len) {
-    uint64_t tag64;
-    if (!rd_varint(r, pos, tag64)) return false;
-    const uint32_t tag = (uint32_t)tag64, field = tag >> 3, wt = tag & 7;
-    if (field == 0) return false;
-    if (depth > 0) {
-      if (wt == 4) {
-        if (stack[depth - 1] != field) return false;
-        depth--;
-        continue;
-      }
-    } else {
-      if (tag == 10) {
-        if (!rd_string(r, pos, ooff, olen)) return false;
-        continue;
-      }
-      if (tag == 16 || tag == 24 || tag == 40) {
-        uint64_t v;
-        if (!rd_varint(r, pos, v)) return false;
-        if (tag == 16) t = (int64_t)v;
-        continue;
-      }
-      if (tag == 34) {
-        if (!rd_string(r, pos, hoff, hlen)) return false;
-        continue;
-      }
-    }
-    switch (wt) {
-      case 0: {
-        uint64_t v;
-        if (!rd_varint(r, pos, v)) return false;
-        break;
-      }
-      case 1:
-        if (r.len - pos < 8) return false;
-        pos += 8;
-        break;
-      case 2: {
-        uint64_t l;
-        if (!rd_varint(r, pos, l)) return false;
-        const int32_t l32 = (int32_t)(uint32_t)l;
-        if (l32 < 0 || (uint32_t)l32 > r.len - pos) return false;
-        pos += (uint32_t)l32;
-        break;
-      }
-      case 3:
-        if (depth >= kMaxGroupDepth) return false;
-        stack[depth++] = field;
-        break;
-      case 5:
-        if (r.len - pos < 4) return false;
-        pos += 4;
-        break;
-      default:  // 4 (END_GROUP at top level), 6, 7
-        return false;
-    }
-  }
-  if (depth != 0) return false;
-  ts = t;
-  hash_off = hoff;
-  hash_len = hlen;
-  return true;
-}
 
 // ---------------------------------------------------------------------------
 // SHA-256 (FIPS 180-4) over one lane's grant bytes.

@@ -1,0 +1,638 @@
+// w2_decode.hip — Write2ToServer wire messages -> the SoA certificate batch,
+// on the device (one lane per message).
+//
+//   k_w2_count  validate the whole message the way protobuf-java's parser
+//               would (any malformation -> MOCHI_MSG_MALFORMED), apply the
+//               fast-path limits (MOCHI_MSG_FALLBACK) and count the grants and
+//               operations the message contributes
+//   (scan)      hipcub exclusive sums -> cert_grant_off / cert_op_off
+//   k_w2_emit   re-walk the message and write grant offsets (zero copy into
+//               the wire blob), signatures, signers, key slots, ops
+//   k_w2_fixup  after the verify path: MALFORMED / FALLBACK / OPS_MISMATCH
+//               messages get their reason code and no accept bit
+//
+// Semantics (restated from protobuf-java 3.16.3, pinned by
+// tests/golden/write2_vectors.json and oracle/mochi_oracle.c):
+//   * message schema MochiProtocol.proto:107-147 + MultiGrant.grantSignatures
+//     = 5 (map<string, bytes>);
+//   * singular scalar / string fields: last value wins; unknown fields and
+//     known fields with a foreign wire type are skipped;
+//   * map fields (WriteCertificate.grants, MultiGrant.grants,
+//     MultiGrant.grantSignatures): entries go into a LinkedHashMap, a repeated
+//     key keeps its FIRST position and takes the LAST value (MapField +
+//     MapEntryLite.parseEntry);
+//   * proto3 strings and string map keys must be valid UTF-8; every Grant
+//     value must parse, including values a later entry replaces.
+// Map de-duplication is done by re-scanning (no per-lane tables): messages
+// hold a handful of MultiGrants and grants, so O(n^2) short compares are
+// cheaper than spilling per-lane maps.
+#include <hipcub/hipcub.hpp>
+
+#include "../../include/mochi_hip.h"
+#include "kernels.h"
+#include "proto_dev.h"
+
+namespace mochi {
+namespace {
+
+constexpr uint32_t kMaxMG = 32;           // MultiGrants per certificate (fast path)
+constexpr uint32_t kMaxGrantsPerMG = 64;  // grants per MultiGrant (fast path)
+constexpr uint32_t kMaxOps = MOCHI_MAX_OPS_PER_CERT;
+
+struct Fld {
+  uint32_t field, wt;
+  uint64_t v;
+  uint32_t off, len;  // wt 2 payload (message-relative)
+};
+
+__device__ __forceinline__ bool vint(ByteReader& r, uint32_t& pos, uint32_t end, uint64_t& v) {
+  uint64_t x = 0;
+#pragma unroll 1
+  for (int i = 0; i < 10; i++) {
+    if (pos >= end) return false;
+    const uint32_t c = r.at(pos++);
+    x |= (uint64_t)(c & 0x7F) << (7 * i);
+    if (!(c & 0x80)) {
+      v = x;
+      return true;
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool vlen(ByteReader& r, uint32_t& pos, uint32_t end, uint32_t& len) {
+  uint64_t l;
+  if (!vint(r, pos, end, l)) return false;
+  const int32_t l32 = (int32_t)(uint32_t)l;  // readRawVarint32
+  if (l32 < 0 || (uint32_t)l32 > end - pos) return false;
+  len = (uint32_t)l32;
+  return true;
+}
+
+// Skip an unknown group opened by `field` (skipMessage + checkLastTagWas).
+__device__ bool skip_group(ByteReader& r, uint32_t& pos, uint32_t end, uint32_t field) {
+  uint32_t stack[kMaxGroupDepth];
+  int depth = 1;
+  stack[0] = field;
+#pragma unroll 1
+  while (depth > 0) {
+    uint64_t t64;
+    if (!vint(r, pos, end, t64)) return false;
+    const uint32_t t = (uint32_t)t64, f = t >> 3, wt = t & 7;
+    if (f == 0) return false;
+    uint32_t l;
+    switch (wt) {
+      case 0: {
+        uint64_t v;
+        if (!vint(r, pos, end, v)) return false;
+        break;
+      }
+      case 1:
+        if (end - pos < 8) return false;
+        pos += 8;
+        break;
+      case 2:
+        if (!vlen(r, pos, end, l)) return false;
+        pos += l;
+        break;
+      case 3:
+        if (depth >= kMaxGroupDepth) return false;
+        stack[depth++] = f;
+        break;
+      case 4:
+        if (stack[depth - 1] != f) return false;
+        depth--;
+        break;
+      case 5:
+        if (end - pos < 4) return false;
+        pos += 4;
+        break;
+      default:
+        return false;
+    }
+  }
+  return true;
+}
+
+// Next field in [pos, end): 1 field, 0 end, -1 malformed.
+__device__ int next_fld(ByteReader& r, uint32_t& pos, uint32_t end, Fld& f) {
+  if (pos >= end) return 0;
+  uint64_t t64;
+  if (!vint(r, pos, end, t64)) return -1;
+  const uint32_t t = (uint32_t)t64;
+  f.field = t >> 3;
+  f.wt = t & 7;
+  f.off = f.len = 0;
+  f.v = 0;
+  if (f.field == 0) return -1;
+  switch (f.wt) {
+    case 0:
+      return vint(r, pos, end, f.v) ? 1 : -1;
+    case 1:
+      if (end - pos < 8) return -1;
+      pos += 8;
+      return 1;
+    case 2:
+      if (!vlen(r, pos, end, f.len)) return -1;
+      f.off = pos;
+      pos += f.len;
+      return 1;
+    case 3:
+      return skip_group(r, pos, end, f.field) ? 1 : -1;
+    case 5:
+      if (end - pos < 4) return -1;
+      pos += 4;
+      return 1;
+    default:
+      return -1;  // END_GROUP at message level, wire types 6 and 7
+  }
+}
+
+// ---- validity: what protobuf-java's parser checks ---------------------------
+__device__ bool valid_grant_at(ByteReader& r, uint32_t off, uint32_t len) {
+  ByteReader g;
+  g.init(r.base + off, len);
+  int64_t ts;
+  uint32_t ho, hl;
+  return parse_grant(g, ts, ho, hl);
+}
+
+// map<string, V> entry; kind 0 = bytes value, 1 = Grant value
+__device__ bool valid_leaf_entry(ByteReader& r, uint32_t off, uint32_t len, int kind) {
+  uint32_t pos = off, end = off + len;
+  Fld f;
+  int rc;
+#pragma unroll 1
+  while ((rc = next_fld(r, pos, end, f)) > 0) {
+    if (f.wt != 2) continue;
+    if (f.field == 1 && !valid_utf8(r, f.off, f.len)) return false;
+    if (f.field == 2 && kind == 1 && !valid_grant_at(r, f.off, f.len)) return false;
+  }
+  return rc == 0;
+}
+
+__device__ bool valid_multigrant(ByteReader& r, uint32_t off, uint32_t len) {
+  uint32_t pos = off, end = off + len;
+  Fld f;
+  int rc;
+#pragma unroll 1
+  while ((rc = next_fld(r, pos, end, f)) > 0) {
+    if (f.wt != 2) continue;
+    if (f.field == 1 && !valid_leaf_entry(r, f.off, f.len, 1)) return false;
+    if (f.field >= 2 && f.field <= 4 && !valid_utf8(r, f.off, f.len)) return false;
+    if (f.field == 5 && !valid_leaf_entry(r, f.off, f.len, 0)) return false;
+  }
+  return rc == 0;
+}
+
+__device__ bool valid_cert_entry(ByteReader& r, uint32_t off, uint32_t len) {
+  uint32_t pos = off, end = off + len;
+  Fld f;
+  int rc;
+#pragma unroll 1
+  while ((rc = next_fld(r, pos, end, f)) > 0) {
+    if (f.wt != 2) continue;
+    if (f.field == 1 && !valid_utf8(r, f.off, f.len)) return false;
+    if (f.field == 2 && !valid_multigrant(r, f.off, f.len)) return false;
+  }
+  return rc == 0;
+}
+
+// every field of `off,len` numbered `field` with wt 2 must satisfy `ok`
+template <typename F>
+__device__ bool all_ld(ByteReader& r, uint32_t off, uint32_t len, uint32_t field, F&& ok) {
+  uint32_t pos = off, end = off + len;
+  Fld f;
+  int rc;
+#pragma unroll 1
+  while ((rc = next_fld(r, pos, end, f)) > 0)
+    if (f.field == field && f.wt == 2 && !ok(f)) return false;
+  return rc == 0;
+}
+
+__device__ bool valid_operation(ByteReader& r, uint32_t off, uint32_t len) {
+  uint32_t pos = off, end = off + len;
+  Fld f;
+  int rc;
+#pragma unroll 1
+  while ((rc = next_fld(r, pos, end, f)) > 0)
+    if (f.wt == 2 && f.field >= 2 && f.field <= 4 && !valid_utf8(r, f.off, f.len)) return false;
+  return rc == 0;
+}
+
+__device__ bool valid_write2(ByteReader& r) {
+  uint32_t pos = 0, end = r.len;
+  Fld f;
+  int rc;
+#pragma unroll 1
+  while ((rc = next_fld(r, pos, end, f)) > 0) {
+    if (f.wt != 2) continue;
+    if (f.field == 1 &&
+        !all_ld(r, f.off, f.len, 1, [&](const Fld& e) { return valid_cert_entry(r, e.off, e.len); }))
+      return false;
+    if (f.field == 2 &&
+        !all_ld(r, f.off, f.len, 1, [&](const Fld& o) { return valid_operation(r, o.off, o.len); }))
+      return false;
+  }
+  return rc == 0;
+}
+
+// ---- extraction on a valid message -------------------------------------------
+struct Entry {
+  uint32_t koff, klen;  // key (last occurrence; default "")
+  uint32_t voff, vlen;  // value (last occurrence; default empty)
+  uint32_t nval;
+};
+
+__device__ void read_entry(ByteReader& r, uint32_t off, uint32_t len, Entry& e) {
+  e.koff = e.klen = e.voff = e.vlen = e.nval = 0;
+  uint32_t pos = off, end = off + len;
+  Fld f;
+#pragma unroll 1
+  while (next_fld(r, pos, end, f) > 0) {
+    if (f.wt != 2) continue;
+    if (f.field == 1) {
+      e.koff = f.off;
+      e.klen = f.len;
+    } else if (f.field == 2) {
+      e.voff = f.off;
+      e.vlen = f.len;
+      e.nval++;
+    }
+  }
+}
+
+// 4 bytes at message offset o (any alignment; o + 4 <= message length)
+__device__ __forceinline__ uint32_t ld4(const uint8_t* base, uint32_t o) {
+  const uintptr_t a = (uintptr_t)(base + o);
+  const uint32_t* wp = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t w0 = wp[0];
+  const uint32_t w1 = sh ? wp[1] : 0u;  // holds byte o+3 when sh != 0
+  return (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh));
+}
+
+// bytes [a, a+n) of message A equal bytes [b, b+n) of message B
+__device__ bool bytes_eq(const uint8_t* A, uint32_t a, const uint8_t* B, uint32_t b, uint32_t n) {
+  uint32_t i = 0;
+#pragma unroll 1
+  for (; i + 4 <= n; i += 4)
+    if (ld4(A, a + i) != ld4(B, b + i)) return false;
+#pragma unroll 1
+  for (; i < n; i++)
+    if (A[a + i] != B[b + i]) return false;
+  return true;
+}
+
+__device__ __forceinline__ bool key_eq(ByteReader& r, uint32_t a, uint32_t al, uint32_t b, uint32_t bl) {
+  return al == bl && (a == b || bytes_eq(r.base, a, r.base, b, al));
+}
+
+// Walk the map entries (field `field`, wt 2) of [off, off+len) in wire order.
+// For entry i that is the FIRST occurrence of its key, fn(first, last) is
+// called with the entry itself and the entry holding the key's final value.
+// Returns false if any entry carries its value more than once (fast-path exit).
+template <typename F>
+__device__ bool for_map(ByteReader& r, uint32_t off, uint32_t len, uint32_t field, F&& fn) {
+  uint32_t pos = off, end = off + len;
+  Fld f;
+#pragma unroll 1
+  while (next_fld(r, pos, end, f) > 0) {
+    if (f.field != field || f.wt != 2) continue;
+    Entry e;
+    read_entry(r, f.off, f.len, e);
+    if (e.nval > 1) return false;
+    // an earlier entry with the same key?
+    bool first = true;
+    {
+      uint32_t p2 = off;
+      Fld g;
+#pragma unroll 1
+      while (p2 < f.off && next_fld(r, p2, end, g) > 0) {
+        if (g.field != field || g.wt != 2 || g.off >= f.off) continue;
+        Entry x;
+        read_entry(r, g.off, g.len, x);
+        if (key_eq(r, x.koff, x.klen, e.koff, e.klen)) {
+          first = false;
+          break;
+        }
+      }
+    }
+    if (!first) continue;
+    Entry last = e;
+    {
+      uint32_t p2 = pos;  // entries after this one
+      Fld g;
+#pragma unroll 1
+      while (next_fld(r, p2, end, g) > 0) {
+        if (g.field != field || g.wt != 2) continue;
+        Entry x;
+        read_entry(r, g.off, g.len, x);
+        if (key_eq(r, x.koff, x.klen, e.koff, e.klen)) last = x;
+      }
+    }
+    if (!fn(e, last)) return false;
+  }
+  return true;
+}
+
+__device__ void last_string(ByteReader& r, uint32_t off, uint32_t len, uint32_t field, uint32_t& so, uint32_t& sl) {
+  so = sl = 0;
+  uint32_t pos = off, end = off + len;
+  Fld f;
+#pragma unroll 1
+  while (next_fld(r, pos, end, f) > 0)
+    if (f.field == field && f.wt == 2) {
+      so = f.off;
+      sl = f.len;
+    }
+}
+
+// Varint at [pos, end) is the minimal encoding of its value.
+__device__ bool canon_varint(ByteReader& r, uint32_t& pos, uint32_t end, uint64_t& v) {
+  const uint32_t p0 = pos;
+  if (!vint(r, pos, end, v)) return false;
+  const uint32_t n = pos - p0;
+  if (n > 1 && r.at(pos - 1) == 0) return false;   // trailing zero group
+  if (n == 10 && r.at(pos - 1) > 1) return false;  // bits beyond 64
+  return true;
+}
+
+// The Grant bytes at [off, off+len) are exactly Grant.toByteArray() of the
+// Grant they parse to (MochiProtocol.java:7556-7574): fields 1..5 in order,
+// each at most once, none at its default, minimal varints, no unknown fields.
+// (Parse validity was checked by valid_write2.)
+__device__ bool grant_canonical(ByteReader& r, uint32_t off, uint32_t len) {
+  uint32_t pos = off, end = off + len, last = 0;
+#pragma unroll 1
+  while (pos < end) {
+    const uint32_t tag = r.at(pos++);  // fields 1..5 have one-byte tags
+    const uint32_t field = tag >> 3, wt = tag & 7;
+    if (field <= last || field > 5) return false;
+    last = field;
+    uint64_t v;
+    if (field == 1 || field == 4) {
+      if (wt != 2) return false;
+      if (!canon_varint(r, pos, end, v) || v == 0 || v > end - pos) return false;
+      pos += (uint32_t)v;
+    } else {
+      if (wt != 0) return false;
+      if (!canon_varint(r, pos, end, v) || v == 0) return false;
+      // enum status: writeEnum writes the int32 sign-extended
+      if (field == 5 && (int64_t)v != (int64_t)(int32_t)(uint32_t)v) return false;
+    }
+  }
+  return true;
+}
+
+// Decode one valid message.  COUNT: returns status and counts.  EMIT: writes
+// outputs at g_base / o_base.  Mirrors oracle/mochi_oracle.c decode_one.
+struct W2Out {
+  uint64_t* grant_off;
+  uint32_t* grant_len;
+  uint8_t* sig;
+  uint16_t* signer;
+  uint8_t* grant_key;
+  uint8_t* op_key;
+  uint8_t* op_flags;
+};
+
+template <bool EMIT>
+__device__ uint32_t decode_msg(ByteReader& r, uint64_t msg_off, const uint8_t* __restrict__ ids,
+                               const uint32_t* __restrict__ id_off, uint32_t n_ids, uint32_t& n_grants,
+                               uint32_t& n_ops, uint32_t g_base, uint32_t o_base, const uint8_t* flags_in,
+                               const W2Out& out) {
+  uint32_t wc_off = 0, wc_len = 0, tx_off = 0, tx_len = 0, n_wc = 0, n_tx = 0;
+  {
+    uint32_t pos = 0;
+    Fld f;
+#pragma unroll 1
+    while (next_fld(r, pos, r.len, f) > 0) {
+      if (f.wt != 2) continue;
+      if (f.field == 1) {
+        wc_off = f.off;
+        wc_len = f.len;
+        n_wc++;
+      } else if (f.field == 2) {
+        tx_off = f.off;
+        tx_len = f.len;
+        n_tx++;
+      }
+    }
+  }
+  if (n_wc > 1 || n_tx > 1) return MOCHI_MSG_FALLBACK;
+  // operations: key slot = index of the first op naming the same operand1
+  uint32_t no = 0;
+  {
+    uint32_t pos = tx_off, end = tx_off + tx_len;
+    Fld f;
+#pragma unroll 1
+    while (next_fld(r, pos, end, f) > 0) {
+      if (f.field != 1 || f.wt != 2) continue;
+      if (no == kMaxOps) return MOCHI_MSG_FALLBACK;
+      if (EMIT) {
+        uint32_t ko, kl;
+        last_string(r, f.off, f.len, 2, ko, kl);
+        uint32_t slot = no, j = 0, p2 = tx_off;
+        Fld g;
+#pragma unroll 1
+        while (j < no && next_fld(r, p2, end, g) > 0) {
+          if (g.field != 1 || g.wt != 2) continue;
+          uint32_t jo, jl;
+          last_string(r, g.off, g.len, 2, jo, jl);
+          if (key_eq(r, jo, jl, ko, kl)) {
+            slot = out.op_key[o_base + j];
+            break;
+          }
+          j++;
+        }
+        out.op_key[o_base + no] = (uint8_t)slot;
+        out.op_flags[o_base + no] = flags_in ? flags_in[no] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
+      }
+      no++;
+    }
+  }
+  n_ops = no;
+  // certificate entries -> MultiGrants -> grants
+  uint32_t n_mg = 0, ng = 0;
+  uint32_t status = MOCHI_MSG_OK;
+  const bool ok = for_map(r, wc_off, wc_len, 1, [&](const Entry&, const Entry& mgv) -> bool {
+    if (++n_mg > kMaxMG) return false;
+    const uint32_t mo = mgv.voff, ml = mgv.vlen;
+    uint16_t signer = 0xFFFF;
+    if (EMIT) {
+      uint32_t so, sl;
+      last_string(r, mo, ml, 4, so, sl);  // MultiGrant.serverId
+#pragma unroll 1
+      for (uint32_t k = 0; k < n_ids; k++)
+        if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) {
+          signer = (uint16_t)k;
+          break;
+        }
+    }
+    uint32_t n_g = 0;
+    return for_map(r, mo, ml, 1, [&](const Entry& ge, const Entry& gv) -> bool {
+      if (++n_g > kMaxGrantsPerMG) return false;
+      if (!EMIT) {
+        if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
+        ng++;
+        return true;
+      }
+      const uint32_t g = g_base + ng++;
+      out.grant_off[g] = msg_off + gv.voff;
+      out.grant_len[g] = gv.vlen;
+      out.signer[g] = signer;
+      // grantSignatures[key]: the last entry with this key, its (last) value
+      uint32_t s_off = 0, s_len = 0;
+      bool have = false;
+      {
+        uint32_t pos = mo, end = mo + ml;
+        Fld f;
+#pragma unroll 1
+        while (next_fld(r, pos, end, f) > 0) {
+          if (f.field != 5 || f.wt != 2) continue;
+          Entry se;
+          read_entry(r, f.off, f.len, se);
+          if (key_eq(r, se.koff, se.klen, ge.koff, ge.klen)) {
+            have = true;
+            s_off = se.voff;
+            s_len = se.vlen;
+          }
+        }
+      }
+      uint4* dst = (uint4*)(out.sig + (size_t)g * MOCHI_RSA_BYTES);
+      if (have && s_len == MOCHI_RSA_BYTES) {
+#pragma unroll 4
+        for (int q = 0; q < 16; q++)
+          dst[q] = make_uint4(ld4(r.base, s_off + 16 * q), ld4(r.base, s_off + 16 * q + 4),
+                              ld4(r.base, s_off + 16 * q + 8), ld4(r.base, s_off + 16 * q + 12));
+      } else {
+#pragma unroll 4
+        for (int q = 0; q < 16; q++) dst[q] = make_uint4(0, 0, 0, 0);
+      }
+      // key slot of the first op naming this grant's key
+      uint8_t key = 0xFF;
+      {
+        uint32_t pos = tx_off, end = tx_off + tx_len, j = 0;
+        Fld f;
+#pragma unroll 1
+        while (next_fld(r, pos, end, f) > 0) {
+          if (f.field != 1 || f.wt != 2) continue;
+          uint32_t ko, kl;
+          last_string(r, f.off, f.len, 2, ko, kl);
+          if (key_eq(r, ko, kl, ge.koff, ge.klen)) {
+            key = out.op_key[o_base + j];
+            break;
+          }
+          j++;
+        }
+      }
+      out.grant_key[g] = key;
+      return true;
+    });
+  });
+  if (!ok) status = MOCHI_MSG_FALLBACK;
+  n_grants = ng;
+  return status;
+}
+
+__global__ __launch_bounds__(256) void k_w2_count(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                                  const uint32_t* __restrict__ mlen, uint32_t M,
+                                                  const uint32_t* __restrict__ flags_off,
+                                                  uint32_t* __restrict__ cnt_g, uint32_t* __restrict__ cnt_o,
+                                                  uint8_t* __restrict__ status) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m > M) return;
+  if (m == M) {  // the scan's extra element: totals land at [M]
+    cnt_g[M] = 0;
+    cnt_o[M] = 0;
+    return;
+  }
+  ByteReader r;
+  r.init(wire + moff[m], mlen[m]);
+  uint32_t ng = 0, no = 0, st;
+  if (!valid_write2(r)) {
+    st = MOCHI_MSG_MALFORMED;
+  } else {
+    W2Out none{};
+    st = decode_msg<false>(r, moff[m], nullptr, nullptr, 0, ng, no, 0, 0, nullptr, none);
+    if (st == MOCHI_MSG_OK && flags_off && flags_off[m + 1] - flags_off[m] != no) st = MOCHI_MSG_OPS_MISMATCH;
+  }
+  if (st != MOCHI_MSG_OK) ng = no = 0;
+  cnt_g[m] = ng;
+  cnt_o[m] = no;
+  status[m] = (uint8_t)st;
+}
+
+__global__ __launch_bounds__(256) void k_w2_emit(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                                 const uint32_t* __restrict__ mlen, uint32_t M,
+                                                 const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off,
+                                                 uint32_t n_ids, const uint32_t* __restrict__ flags_off,
+                                                 const uint8_t* __restrict__ flags_in,
+                                                 const uint32_t* __restrict__ g_base,
+                                                 const uint32_t* __restrict__ o_base,
+                                                 const uint8_t* __restrict__ status, W2Out out) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M || status[m] != MOCHI_MSG_OK) return;
+  ByteReader r;
+  r.init(wire + moff[m], mlen[m]);
+  uint32_t ng, no;
+  decode_msg<true>(r, moff[m], ids, id_off, n_ids, ng, no, g_base[m], o_base[m],
+                   flags_off ? flags_in + flags_off[m] : nullptr, out);
+}
+
+__global__ __launch_bounds__(256) void k_w2_fixup(const uint8_t* __restrict__ status, uint32_t M,
+                                                  uint32_t* __restrict__ accept_bits, uint8_t* __restrict__ reason,
+                                                  uint8_t* __restrict__ fail_op) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool bad = m < M && status[m] != MOCHI_MSG_OK;
+  const uint64_t badmask = __ballot(bad);
+  if (m < M && bad) {
+    if (reason) reason[m] = status[m] == MOCHI_MSG_MALFORMED ? MOCHI_REJECT_MALFORMED : MOCHI_UNDECIDED;
+    if (fail_op) fail_op[m] = 0xFF;
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wbase = (m - lane) >> 5, nwords = (M + 31) >> 5;
+  if (lane == 0 && badmask) {
+    if (wbase < nwords) accept_bits[wbase] &= ~(uint32_t)badmask;
+    if (wbase + 1 < nwords) accept_bits[wbase + 1] &= ~(uint32_t)(badmask >> 32);
+  }
+}
+
+inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+
+}  // namespace
+
+hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes) {
+  return hipcub::DeviceScan::ExclusiveSum(nullptr, *bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+}
+
+hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_w2_count, dim3(cdiv((uint64_t)a.M + 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len,
+                     a.M, a.flags_off, a.cnt_g, a.cnt_o, a.status);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  size_t tb = a.scan_temp_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_g, a.cert_grant_off, (int)(a.M + 1), st);
+  if (e != hipSuccess) return e;
+  tb = a.scan_temp_bytes;
+  return hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_o, a.cert_op_off, (int)(a.M + 1), st);
+}
+
+hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
+  W2Out o{a.grant_off, a.grant_len, a.sig, a.signer, a.grant_key, a.op_key, a.op_flags};
+  if (a.M)
+    hipLaunchKernelGGL(k_w2_emit, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, a.ids,
+                       a.id_off, a.n_ids, a.flags_off, a.flags_in, a.cert_grant_off, a.cert_op_off, a.status, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reason, uint8_t* fail_op,
+                           hipStream_t st) {
+  if (a.M)
+    hipLaunchKernelGGL(k_w2_fixup, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.status, a.M, accept_bits, reason,
+                       fail_op);
+  return hipGetLastError();
+}
+
+}  // namespace mochi

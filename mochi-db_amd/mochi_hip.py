@@ -141,6 +141,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mochi_ctx_last_total_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     lib.mochi_ctx_set_chunk_grants.argtypes = [vp, u32]
+    lib.mochi_ctx_set_server_ids.argtypes = [vp, vp, vp, u32]
+    lib.mochi_verify_write2.argtypes = [vp, vp, vp, vp, vp]
+    lib.mochi_verify_write2_device.argtypes = [vp, vp, vp, vp, vp, vp]
+    lib.mochi_write2_decode.argtypes = [vp, vp, vp]
+    lib.mochi_write2_decoded_free.argtypes = [vp]
     lib.mochi_host_alloc.restype = vp
     lib.mochi_host_alloc.argtypes = [ctypes.c_uint64]
     lib.mochi_host_free.argtypes = [vp]
@@ -335,6 +340,57 @@ class Verifier:
         if not self.ctx:
             raise MochiError(f"mochi_ctx_create failed: {_err(self.lib)}")
         self.device = device
+
+    def set_server_ids(self, server_ids) -> None:
+        """Key i of the table belongs to MultiGrant.serverId == server_ids[i] (Write2 wire path)."""
+        enc = [x.encode() if isinstance(x, str) else bytes(x) for x in server_ids]
+        blob = np.frombuffer(b"".join(enc) or b"\x00", np.uint8).copy()
+        off = np.zeros(len(enc) + 1, np.uint32)
+        np.cumsum([len(x) for x in enc], out=off[1:])
+        if self.lib.mochi_ctx_set_server_ids(self.ctx, _ptr(blob), _ptr(off), len(enc)) != OK:
+            raise MochiError(f"mochi_ctx_set_server_ids: {_err(self.lib)}")
+
+    def verify_write2(self, wb, replication_factor: int, strict_gt: bool = True):
+        """Write2ToServer messages (workload.WireBatch, host memory) -> (Verdicts with
+        certificate-level arrays, msg_status[M])."""
+        wc, keep = write2_batch_c(wb)
+        M = wb.n_msgs
+        out = Verdicts.alloc(0, M)
+        vc = out.to_c()
+        vc.grant_valid_bits = vc.grant_flags = vc.grant_ts = None
+        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        st = np.zeros(max(M, 1), np.uint8)
+        rc = self.lib.mochi_verify_write2(self.ctx, ctypes.addressof(wc), ctypes.addressof(p), ctypes.addressof(vc),
+                                          _ptr(st))
+        if rc != OK:
+            raise MochiError(f"mochi_verify_write2 rc={rc}: {_err(self.lib)}")
+        t = ctypes.c_float()
+        self.lib.mochi_ctx_last_total_ms(self.ctx, ctypes.byref(t))
+        out.timing_ms = {"total": t.value}
+        return out, st[:M].copy()
+
+    def decode_write2(self, wb) -> dict:
+        """The device decoder's SoA view of the messages (inspection / tests)."""
+        wc, keep = write2_batch_c(wb)
+        d = Write2Decoded_C()
+        rc = self.lib.mochi_write2_decode(self.ctx, ctypes.addressof(wc), ctypes.addressof(d))
+        if rc != OK:
+            raise MochiError(f"mochi_write2_decode rc={rc}: {_err(self.lib)}")
+        N, M, O = d.n_grants, d.n_msgs, d.n_ops
+
+        def arr(ptr, n, dt):
+            if n == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         shape=(n,)).copy()
+
+        out = dict(grant_off=arr(d.grant_off, N, np.uint64), grant_len=arr(d.grant_len, N, np.uint32),
+                   sig=arr(d.sig, N * 256, np.uint8).reshape(N, 256), signer=arr(d.signer, N, np.uint16),
+                   grant_key=arr(d.grant_key, N, np.uint8), cert_grant_off=arr(d.cert_grant_off, M + 1, np.uint32),
+                   cert_op_off=arr(d.cert_op_off, M + 1, np.uint32), op_key=arr(d.op_key, O, np.uint8),
+                   op_flags=arr(d.op_flags, O, np.uint8), msg_status=arr(d.msg_status, M, np.uint8))
+        self.lib.mochi_write2_decoded_free(ctypes.addressof(d))
+        return out
 
     def set_chunk_grants(self, grants: int) -> None:
         """Host-path pipeline chunk target (grants); 0 restores the default."""
@@ -594,4 +650,46 @@ def write1_classify(requests) -> np.ndarray:
     if rc != OK:
         raise MochiError(f"mochi_write1_classify: {_err(lib)}")
     return out[:len(requests)].copy()
+
+
+class Write2Batch_C(ctypes.Structure):
+    _fields_ = [
+        ("n_msgs", ctypes.c_uint32),
+        ("_pad0", ctypes.c_uint32),
+        ("wire_len", ctypes.c_uint64),
+        ("wire", ctypes.c_void_p),
+        ("msg_off", ctypes.c_void_p),
+        ("msg_len", ctypes.c_void_p),
+        ("op_flags_off", ctypes.c_void_p),
+        ("op_flags", ctypes.c_void_p),
+        ("expected_hash", ctypes.c_void_p),
+    ]
+
+
+MSG_OK, MSG_MALFORMED, MSG_FALLBACK, MSG_OPS_MISMATCH = 0, 1, 2, 3
+UNDECIDED = 7
+REASON_NAMES[UNDECIDED] = "UNDECIDED"
+
+
+def write2_batch_c(wb):
+    """workload.WireBatch (host arrays) -> (Write2Batch_C, keep-alive list)."""
+    arrs = [np.ascontiguousarray(wb.wire, np.uint8), np.ascontiguousarray(wb.msg_off, np.uint64),
+            np.ascontiguousarray(wb.msg_len, np.uint32),
+            None if wb.op_flags_off is None else np.ascontiguousarray(wb.op_flags_off, np.uint32),
+            np.ascontiguousarray(wb.op_flags if wb.op_flags.size else np.zeros(1, np.uint8), np.uint8),
+            np.ascontiguousarray(wb.expected_hash, np.uint8).reshape(-1)]
+    c = Write2Batch_C()
+    c.n_msgs = int(arrs[1].shape[0])
+    c.wire_len = int(arrs[0].nbytes)
+    c.wire, c.msg_off, c.msg_len = _ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2])
+    c.op_flags_off, c.op_flags, c.expected_hash = _ptr(arrs[3]), _ptr(arrs[4]), _ptr(arrs[5])
+    return c, arrs
+
+
+class Write2Decoded_C(ctypes.Structure):
+    _fields_ = [("n_msgs", ctypes.c_uint32), ("n_grants", ctypes.c_uint32), ("n_ops", ctypes.c_uint32),
+                ("_pad0", ctypes.c_uint32), ("grant_off", ctypes.c_void_p), ("grant_len", ctypes.c_void_p),
+                ("sig", ctypes.c_void_p), ("signer", ctypes.c_void_p), ("grant_key", ctypes.c_void_p),
+                ("cert_grant_off", ctypes.c_void_p), ("cert_op_off", ctypes.c_void_p), ("op_key", ctypes.c_void_p),
+                ("op_flags", ctypes.c_void_p), ("msg_status", ctypes.c_void_p)]
 

@@ -254,3 +254,143 @@ def make_batch(pool: Pool, n_certs: int, first_cert: int = 0, seed: int = SEED, 
 
 def n_certs_for_grants(n_grants: int, R: int, k: int = 1) -> int:
     return max(1, n_grants // (R * k))
+
+
+# ---------------------------------------------------------------------------
+# Write2ToServer wire encoding (MochiProtocol.proto:107-147, proto3, field
+# order and map-entry layout as protobuf-java writes them: every map entry
+# carries its key and value, MapEntryLite.writeTo) with the grantSignatures
+# map INTEGRATION.md adds to MultiGrant (field 5).
+# ---------------------------------------------------------------------------
+def _ld(field: int, payload: bytes) -> bytes:
+    return _varint(field << 3 | 2) + _varint(len(payload)) + payload
+
+
+def encode_map_entry(field: int, key: bytes, value: bytes) -> bytes:
+    return _ld(field, _ld(1, key) + _ld(2, value))
+
+
+def encode_multigrant(grants, server_id: str, client_id: str = "", mg_hash: str = "", sigs=None) -> bytes:
+    """grants / sigs: lists of (objectId, bytes) in map insertion order."""
+    out = bytearray()
+    for oid, gb in grants:
+        out += encode_map_entry(1, oid.encode(), gb)
+    if client_id:
+        out += _ld(2, client_id.encode())
+    if mg_hash:
+        out += _ld(3, mg_hash.encode())
+    if server_id:
+        out += _ld(4, server_id.encode())
+    for oid, sig in sigs or []:
+        out += encode_map_entry(5, oid.encode(), sig)
+    return bytes(out)
+
+
+def encode_operation(action: int, operand1: str, operand2: str = "") -> bytes:
+    out = bytearray()
+    if action:
+        out += b"\x08" + _varint(action)
+    if operand1:
+        out += _ld(2, operand1.encode())
+    if operand2:
+        out += _ld(3, operand2.encode())
+    return bytes(out)
+
+
+def encode_write2(multigrants, operations) -> bytes:
+    """multigrants: [(certificate map key = serverId, MultiGrant bytes)], operations: [Operation bytes]."""
+    wc = b"".join(encode_map_entry(1, sid.encode(), mg) for sid, mg in multigrants)
+    txn = b"".join(_ld(1, op) for op in operations)
+    return (_ld(1, wc) if wc else b"") + (_ld(2, txn) if txn else b"")
+
+
+def grant_object_id(gb: bytes) -> str:
+    """objectId of a canonical Grant (field 1 first)."""
+    if not gb or gb[0] != 0x0A:
+        return ""
+    n, i, shift = 0, 1, 0
+    while True:
+        c = gb[i]
+        n |= (c & 0x7F) << shift
+        i += 1
+        if not c & 0x80:
+            break
+        shift += 7
+    return gb[i:i + n].decode()
+
+
+@dataclass
+class WireBatch:
+    """Write2ToServer messages + the host inputs of mochi_write2_batch."""
+
+    wire: np.ndarray  # uint8 blob
+    msg_off: np.ndarray  # uint64 [M]
+    msg_len: np.ndarray  # uint32 [M]
+    op_flags_off: Optional[np.ndarray]  # uint32 [M+1] or None
+    op_flags: np.ndarray  # uint8
+    expected_hash: np.ndarray  # uint8 [M, 128]
+
+    @property
+    def n_msgs(self) -> int:
+        return int(self.msg_off.shape[0])
+
+
+def encode_wire_batch(s: Synth, server_ids=None, client_id: str = "client-7f3a", pad: int = 0) -> WireBatch:
+    """The Write2ToServer messages a MochiDB server would receive for the
+    synthetic certificates of `s`: one MultiGrant per replica in server order
+    (certificate map key = MultiGrant.serverId), grants keyed by objectId with
+    their signatures in grantSignatures, a WRITE operation per op key."""
+    b = s.batch
+    ids = server_ids or SERVER_IDS
+    C = b.n_certs
+    msgs, ops_per = [], []
+    for c in range(C):
+        g0, g1 = int(b.cert_grant_off[c]), int(b.cert_grant_off[c + 1])
+        o0, o1 = int(b.cert_op_off[c]), int(b.cert_op_off[c + 1])
+        oids = {}
+        mgs, cur, cur_r = [], [], None
+        for g in range(g0, g1):
+            gb = b.grant_bytes[int(b.grant_off[g]):int(b.grant_off[g]) + int(b.grant_len[g])].tobytes()
+            oid = grant_object_id(gb)
+            oids[int(b.grant_key[g])] = oid
+            r = int(b.signer[g])
+            if r != cur_r and cur:
+                mgs.append((cur_r, cur))
+                cur = []
+            cur_r = r
+            cur.append((oid, gb, b.sig[g].tobytes()))
+        if cur:
+            mgs.append((cur_r, cur))
+        th = b.expected_hash[c].tobytes().decode()
+        enc = []
+        for r, items in mgs:
+            sid = ids[r] if r < len(ids) else f"server-unknown-{r}"
+            mg = encode_multigrant([(o, gb) for o, gb, _ in items], sid, client_id, th,
+                                   [(o, sg) for o, _, sg in items])
+            enc.append((sid, mg))
+        ops = [encode_operation(2, oids.get(int(b.op_key[o]), f"key-{int(b.op_key[o])}"), f"value-{c}-{o - o0}")
+               for o in range(o0, o1)]
+        msgs.append(encode_write2(enc, ops))
+        ops_per.append(o1 - o0)
+    off = np.zeros(C, np.uint64)
+    pos = 0
+    parts = []
+    for i, m in enumerate(msgs):
+        pos += pad
+        parts.append(b"\xee" * pad)
+        off[i] = pos
+        parts.append(m)
+        pos += len(m)
+    wire = np.frombuffer(b"".join(parts) or b"\x00", np.uint8).copy()
+    ofo = np.zeros(C + 1, np.uint32)
+    np.cumsum(ops_per, out=ofo[1:])
+    return WireBatch(wire=wire, msg_off=off, msg_len=np.array([len(m) for m in msgs], np.uint32),
+                     op_flags_off=ofo, op_flags=b.op_flags.copy(), expected_hash=b.expected_hash.copy())
+
+
+def server_id_table(n: int, server_ids=None):
+    ids = (server_ids or SERVER_IDS)[:n]
+    blob = "".join(ids).encode()
+    off = np.zeros(n + 1, np.uint32)
+    np.cumsum([len(x.encode()) for x in ids], out=off[1:])
+    return np.frombuffer(blob, np.uint8).copy(), off

@@ -697,3 +697,427 @@ int oracle_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const 
   }
   return MOCHI_OK;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Write2ToServer wire decode (MochiProtocol.proto:107-147 + the proposed    */
+/* MultiGrant.grantSignatures = 5), protobuf-java 3.16.3 semantics:           */
+/*   - generated parsers (MochiProtocol.java Write2ToServer / WriteCertificate */
+/*     / MultiGrant / Transaction / Operation constructors) take the LAST      */
+/*     value of a singular scalar/string field, MERGE repeated occurrences of  */
+/*     a singular message field, and skip unknown fields (parseUnknownField);  */
+/*   - map fields: each entry is parsed by MapEntryLite.parseEntry (key and    */
+/*     value last-wins, message values merged, unknown fields skipped) and     */
+/*     put into MapField's LinkedHashMap: a repeated key keeps its FIRST       */
+/*     position and takes the LAST value;                                      */
+/*   - proto3 string fields and string map keys require valid UTF-8;          */
+/*   - any malformation fails the whole message (InvalidProtocolBufferException).*/
+/* The device decoder's fast path (include/mochi_hip.h, MOCHI_MSG_FALLBACK)   */
+/* is restated here too, so the two agree message by message.                 */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+  uint32_t field, wt;
+  uint64_t v;
+  size_t off, len; /* wt 2 payload */
+} fld_t;
+
+static int skip_group(rd_t* r, uint32_t field, int depth) {
+  if (depth > ORACLE_MAX_GROUP_DEPTH) return 0;
+  for (;;) {
+    uint64_t t64, v;
+    if (!rd_varint(r, &t64)) return 0; /* truncated inside the group */
+    const uint32_t t = (uint32_t)t64, f = t >> 3, wt = t & 7;
+    if (f == 0) return 0;
+    switch (wt) {
+      case 0: if (!rd_varint(r, &v)) return 0; break;
+      case 1: if (r->len - r->pos < 8) return 0; r->pos += 8; break;
+      case 2: {
+        if (!rd_varint(r, &v)) return 0;
+        const int32_t l = (int32_t)(uint32_t)v;
+        if (l < 0 || (uint64_t)l > r->len - r->pos) return 0;
+        r->pos += (size_t)l;
+        break;
+      }
+      case 3: if (!skip_group(r, f, depth + 1)) return 0; break;
+      case 4: return f == field; /* checkLastTagWas(END_GROUP of this field) */
+      case 5: if (r->len - r->pos < 4) return 0; r->pos += 4; break;
+      default: return 0;
+    }
+  }
+}
+
+/* Next field of the message being read: 1 field, 0 end, -1 malformed. */
+static int next_fld(rd_t* r, fld_t* f) {
+  if (r->pos >= r->len) return 0;
+  uint64_t t64;
+  if (!rd_varint(r, &t64)) return -1;
+  const uint32_t t = (uint32_t)t64;
+  f->field = t >> 3;
+  f->wt = t & 7;
+  f->off = f->len = 0;
+  f->v = 0;
+  if (f->field == 0) return -1;
+  switch (f->wt) {
+    case 0: return rd_varint(r, &f->v) ? 1 : -1;
+    case 1: if (r->len - r->pos < 8) return -1; r->pos += 8; return 1;
+    case 2: {
+      uint64_t l;
+      if (!rd_varint(r, &l)) return -1;
+      const int32_t l32 = (int32_t)(uint32_t)l;
+      if (l32 < 0 || (uint64_t)l32 > r->len - r->pos) return -1;
+      f->off = r->pos;
+      f->len = (size_t)l32;
+      r->pos += (size_t)l32;
+      return 1;
+    }
+    case 3: return skip_group(r, f->field, 1) ? 1 : -1;
+    case 5: if (r->len - r->pos < 4) return -1; r->pos += 4; return 1;
+    default: return -1; /* END_GROUP at message level, wire types 6, 7 */
+  }
+}
+
+#define FOR_FIELDS(buf, o, l, f, rc)                                   \
+  for (rd_t r_ = {(buf) + (o), (l), 0}; (rc = next_fld(&r_, &f)) > 0;)
+
+/* --- full validity (what protobuf-java's parser checks) --- */
+static int valid_str(const uint8_t* m, const fld_t* f) { return valid_utf8(m + f->off, f->len); }
+
+static int valid_grant_msg(const uint8_t* m, size_t off, size_t len) {
+  oracle_grant_view v;
+  return oracle_grant_parse(m + off, len, &v);
+}
+
+/* map entry with a string key; value validated by `val` (NULL: bytes) */
+static int valid_entry(const uint8_t* m, size_t off, size_t len, int (*val)(const uint8_t*, size_t, size_t)) {
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc) {
+    if (f.field == 1 && f.wt == 2 && !valid_str(m + off, &f)) return 0;
+    if (f.field == 2 && f.wt == 2 && val && !val(m + off, f.off, f.len)) return 0;
+  }
+  return rc == 0;
+}
+
+static int valid_multigrant(const uint8_t* m, size_t off, size_t len) {
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc) {
+    if (f.wt != 2) continue;
+    if (f.field == 1 && !valid_entry(m + off, f.off, f.len, valid_grant_msg)) return 0;
+    if ((f.field == 2 || f.field == 3 || f.field == 4) && !valid_str(m + off, &f)) return 0;
+    if (f.field == 5 && !valid_entry(m + off, f.off, f.len, NULL)) return 0;
+  }
+  return rc == 0;
+}
+
+static int valid_wc(const uint8_t* m, size_t off, size_t len) {
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc)
+    if (f.field == 1 && f.wt == 2 && !valid_entry(m + off, f.off, f.len, valid_multigrant)) return 0;
+  return rc == 0;
+}
+
+static int valid_operation(const uint8_t* m, size_t off, size_t len) {
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc)
+    if (f.field >= 2 && f.field <= 4 && f.wt == 2 && !valid_str(m + off, &f)) return 0;
+  return rc == 0;
+}
+
+static int valid_txn(const uint8_t* m, size_t off, size_t len) {
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc)
+    if (f.field == 1 && f.wt == 2 && !valid_operation(m + off, f.off, f.len)) return 0;
+  return rc == 0;
+}
+
+static int valid_write2(const uint8_t* m, size_t len) {
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, 0, len, f, rc) {
+    if (f.field == 1 && f.wt == 2 && !valid_wc(m, f.off, f.len)) return 0;
+    if (f.field == 2 && f.wt == 2 && !valid_txn(m, f.off, f.len)) return 0;
+  }
+  return rc == 0;
+}
+
+/* --- extraction on a valid message --- */
+typedef struct {
+  size_t koff, klen; /* key (default "") */
+  size_t voff, vlen; /* last value occurrence (default empty) */
+  int nval;          /* value occurrences */
+} entry_t;
+
+static void read_entry(const uint8_t* m, size_t off, size_t len, entry_t* e) {
+  fld_t f;
+  int rc;
+  memset(e, 0, sizeof *e);
+  FOR_FIELDS(m, off, len, f, rc) {
+    if (f.wt != 2) continue;
+    if (f.field == 1) {
+      e->koff = off + f.off;
+      e->klen = f.len;
+    } else if (f.field == 2) {
+      e->voff = off + f.off;
+      e->vlen = f.len;
+      e->nval++;
+    }
+  }
+}
+
+static int same(const uint8_t* m, size_t a, size_t al, size_t b, size_t bl) {
+  return al == bl && memcmp(m + a, m + b, al) == 0;
+}
+
+/* entries of map field `field` in [off, off+len): LinkedHashMap put order.
+ * Returns the number of entries (all of them, before de-duplication). */
+static size_t list_entries(const uint8_t* m, size_t off, size_t len, uint32_t field, entry_t** out) {
+  size_t n = 0, cap = 8;
+  entry_t* v = (entry_t*)malloc(cap * sizeof *v);
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc) {
+    if (f.field != field || f.wt != 2) continue;
+    if (n == cap) v = (entry_t*)realloc(v, (cap *= 2) * sizeof *v);
+    read_entry(m, off + f.off, f.len, &v[n++]);
+  }
+  *out = v;
+  return n;
+}
+
+/* index of the entry holding key i's final value, or -1 if i is not the first occurrence */
+static long map_slot(const uint8_t* m, const entry_t* e, size_t n, size_t i) {
+  for (size_t j = 0; j < i; j++)
+    if (same(m, e[j].koff, e[j].klen, e[i].koff, e[i].klen)) return -1;
+  size_t last = i;
+  for (size_t j = i + 1; j < n; j++)
+    if (same(m, e[j].koff, e[j].klen, e[i].koff, e[i].klen)) last = j;
+  return (long)last;
+}
+
+static void last_string(const uint8_t* m, size_t off, size_t len, uint32_t field, size_t* so, size_t* sl) {
+  fld_t f;
+  int rc;
+  *so = 0;
+  *sl = 0;
+  FOR_FIELDS(m, off, len, f, rc)
+    if (f.field == field && f.wt == 2) {
+      *so = off + f.off;
+      *sl = f.len;
+    }
+}
+
+/* Grant bytes equal to what Grant.toByteArray() gives for the parsed Grant. */
+static int grant_canonical(const uint8_t* g, size_t len) {
+  oracle_grant_view v;
+  if (!oracle_grant_parse(g, len, &v)) return 0;
+  uint8_t buf[1024];
+  if (len > sizeof buf) return 0;
+  const long n = oracle_grant_encode((const char*)g + v.object_id_off, v.object_id_len, v.timestamp, v.configstamp,
+                                     (const char*)g + v.txn_hash_off, v.txn_hash_len, v.status, buf, sizeof buf);
+  return n == (long)len && memcmp(buf, g, len) == 0;
+}
+
+#define W2_MAX_MULTIGRANTS 32
+#define W2_MAX_GRANTS_PER_MG 64
+
+typedef struct {
+  uint32_t n; /* grants emitted so far */
+  uint32_t cap;
+  uint64_t* off;
+  uint32_t* len;
+  uint8_t* sig;
+  uint16_t* signer;
+  uint8_t* key;
+} gout_t;
+
+static void gout_push(gout_t* o, uint64_t off, uint32_t len, const uint8_t* sig, uint16_t signer, uint8_t key) {
+  if (o->n == o->cap) {
+    o->cap = o->cap ? o->cap * 2 : 1024;
+    o->off = (uint64_t*)realloc(o->off, o->cap * sizeof(uint64_t));
+    o->len = (uint32_t*)realloc(o->len, o->cap * sizeof(uint32_t));
+    o->sig = (uint8_t*)realloc(o->sig, (size_t)o->cap * MOCHI_RSA_BYTES);
+    o->signer = (uint16_t*)realloc(o->signer, o->cap * sizeof(uint16_t));
+    o->key = (uint8_t*)realloc(o->key, o->cap);
+  }
+  o->off[o->n] = off;
+  o->len[o->n] = len;
+  if (sig) memcpy(o->sig + (size_t)o->n * MOCHI_RSA_BYTES, sig, MOCHI_RSA_BYTES);
+  else memset(o->sig + (size_t)o->n * MOCHI_RSA_BYTES, 0, MOCHI_RSA_BYTES);
+  o->signer[o->n] = signer;
+  o->key[o->n] = key;
+  o->n++;
+}
+
+/* Decode message m (valid) into grants / ops; returns MOCHI_MSG_OK or MOCHI_MSG_FALLBACK. */
+static int decode_one(const uint8_t* m, size_t mlen, uint64_t base, const uint8_t* ids, const uint32_t* id_off,
+                      uint32_t n_ids, gout_t* go, uint8_t* op_key, uint32_t* n_ops) {
+  fld_t f;
+  int rc;
+  size_t wc_off = 0, wc_len = 0, tx_off = 0, tx_len = 0;
+  int n_wc = 0, n_tx = 0;
+  FOR_FIELDS(m, 0, mlen, f, rc) {
+    if (f.field == 1 && f.wt == 2) { wc_off = f.off; wc_len = f.len; n_wc++; }
+    if (f.field == 2 && f.wt == 2) { tx_off = f.off; tx_len = f.len; n_tx++; }
+  }
+  if (n_wc > 1 || n_tx > 1) return MOCHI_MSG_FALLBACK; /* merged singular message fields */
+  /* operations, transaction order; key slot = first op with the same operand1 */
+  size_t op_o[MOCHI_MAX_OPS_PER_CERT], op_l[MOCHI_MAX_OPS_PER_CERT];
+  uint32_t no = 0;
+  FOR_FIELDS(m, tx_off, tx_len, f, rc) {
+    if (f.field != 1 || f.wt != 2) continue;
+    if (no == MOCHI_MAX_OPS_PER_CERT) return MOCHI_MSG_FALLBACK;
+    last_string(m, tx_off + f.off, f.len, 2, &op_o[no], &op_l[no]);
+    uint32_t slot = no;
+    for (uint32_t j = 0; j < no; j++)
+      if (same(m, op_o[j], op_l[j], op_o[no], op_l[no])) { slot = op_key[j]; break; }
+    op_key[no++] = (uint8_t)slot;
+  }
+  *n_ops = no;
+  /* certificate entries: WriteCertificate.grants (serverId -> MultiGrant) */
+  entry_t* ce;
+  const size_t nce = list_entries(m, wc_off, wc_len, 1, &ce);
+  int status = MOCHI_MSG_OK;
+  uint32_t n_mg = 0;
+  const uint32_t g_start = go->n;
+  for (size_t i = 0; i < nce && status == MOCHI_MSG_OK; i++)
+    if (ce[i].nval > 1) status = MOCHI_MSG_FALLBACK;
+  for (size_t i = 0; i < nce && status == MOCHI_MSG_OK; i++) {
+    const long s = map_slot(m, ce, nce, i);
+    if (s < 0) continue;
+    if (++n_mg > W2_MAX_MULTIGRANTS) { status = MOCHI_MSG_FALLBACK; break; }
+    const size_t mo = ce[s].voff, ml = ce[s].vlen;
+    size_t sid_o, sid_l;
+    last_string(m, mo, ml, 4, &sid_o, &sid_l); /* MultiGrant.serverId */
+    uint16_t signer = 0xFFFF;
+    for (uint32_t k = 0; k < n_ids; k++)
+      if (id_off[k + 1] - id_off[k] == sid_l && memcmp(ids + id_off[k], m + sid_o, sid_l) == 0) { signer = (uint16_t)k; break; }
+    entry_t *ge, *se;
+    const size_t nge = list_entries(m, mo, ml, 1, &ge);
+    const size_t nse = list_entries(m, mo, ml, 5, &se);
+    uint32_t n_g = 0;
+    for (size_t a = 0; a < nge && status == MOCHI_MSG_OK; a++)
+      if (ge[a].nval > 1) status = MOCHI_MSG_FALLBACK;
+    for (size_t a = 0; a < nge && status == MOCHI_MSG_OK; a++) {
+      const long t = map_slot(m, ge, nge, a);
+      if (t < 0) continue;
+      if (++n_g > W2_MAX_GRANTS_PER_MG) { status = MOCHI_MSG_FALLBACK; break; }
+      if (!grant_canonical(m + ge[t].voff, ge[t].vlen)) { status = MOCHI_MSG_FALLBACK; break; }
+      /* grantSignatures[key]: the last entry with this key, its (last) value */
+      const uint8_t* sig = NULL;
+      for (size_t q = 0; q < nse; q++)
+        if (same(m, se[q].koff, se[q].klen, ge[a].koff, ge[a].klen))
+          sig = se[q].vlen == MOCHI_RSA_BYTES ? m + se[q].voff : NULL;
+      uint8_t key = 0xFF;
+      for (uint32_t j = 0; j < no; j++)
+        if (same(m, op_o[j], op_l[j], ge[a].koff, ge[a].klen)) { key = op_key[j]; break; }
+      gout_push(go, base + ge[t].voff, (uint32_t)ge[t].vlen, sig, signer, key);
+    }
+    free(ge);
+    free(se);
+  }
+  free(ce);
+  if (status != MOCHI_MSG_OK) go->n = g_start; /* drop partial output */
+  return status;
+}
+
+int oracle_w2_decode(const mochi_write2_batch* w, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids,
+                     oracle_w2_decoded* out) {
+  if (!w || !out) return MOCHI_EINVAL;
+  memset(out, 0, sizeof *out);
+  const uint32_t M = w->n_msgs;
+  gout_t go;
+  memset(&go, 0, sizeof go);
+  uint32_t* cg = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
+  uint32_t* co = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
+  uint8_t* st = (uint8_t*)calloc(M ? M : 1, 1);
+  size_t ocap = 1024, on = 0;
+  uint8_t* opk = (uint8_t*)malloc(ocap);
+  uint8_t* opf = (uint8_t*)malloc(ocap);
+  for (uint32_t i = 0; i < M; i++) {
+    const uint8_t* m = w->wire + w->msg_off[i];
+    const size_t ml = w->msg_len[i];
+    uint8_t keys[MOCHI_MAX_OPS_PER_CERT];
+    uint32_t no = 0;
+    int s = valid_write2(m, ml) ? decode_one(m, ml, w->msg_off[i], ids, id_off, n_ids, &go, keys, &no)
+                                : MOCHI_MSG_MALFORMED;
+    if (s == MOCHI_MSG_OK && w->op_flags_off && w->op_flags_off[i + 1] - w->op_flags_off[i] != no)
+      s = MOCHI_MSG_OPS_MISMATCH;
+    if (s != MOCHI_MSG_OK) {
+      no = 0;
+      go.n = cg[i];
+    }
+    st[i] = (uint8_t)s;
+    if (on + no > ocap) {
+      while (on + no > ocap) ocap *= 2;
+      opk = (uint8_t*)realloc(opk, ocap);
+      opf = (uint8_t*)realloc(opf, ocap);
+    }
+    for (uint32_t j = 0; j < no; j++) {
+      opk[on + j] = keys[j];
+      opf[on + j] = w->op_flags_off ? w->op_flags[w->op_flags_off[i] + j] : (MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
+    }
+    on += no;
+    cg[i + 1] = go.n;
+    co[i + 1] = (uint32_t)on;
+  }
+  mochi_batch* b = &out->batch;
+  b->n_grants = go.n;
+  b->n_certs = M;
+  b->n_ops = (uint32_t)on;
+  b->grant_bytes_len = w->wire_len;
+  b->grant_bytes = w->wire;
+  b->grant_off = go.off;
+  b->grant_len = go.len;
+  b->sig = go.sig;
+  b->signer = go.signer;
+  b->grant_key = go.key;
+  b->cert_grant_off = cg;
+  b->cert_op_off = co;
+  b->op_key = opk;
+  b->op_flags = opf;
+  b->expected_hash = w->expected_hash;
+  out->msg_status = st;
+  return MOCHI_OK;
+}
+
+void oracle_w2_free(oracle_w2_decoded* d) {
+  if (!d) return;
+  free((void*)d->batch.grant_off);
+  free((void*)d->batch.grant_len);
+  free((void*)d->batch.sig);
+  free((void*)d->batch.signer);
+  free((void*)d->batch.grant_key);
+  free((void*)d->batch.cert_grant_off);
+  free((void*)d->batch.cert_op_off);
+  free((void*)d->batch.op_key);
+  free((void*)d->batch.op_flags);
+  free(d->msg_status);
+  memset(d, 0, sizeof *d);
+}
+
+int oracle_verify_write2(const uint8_t* moduli_be, uint32_t n_keys, const uint8_t* ids, const uint32_t* id_off,
+                         const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* out, uint8_t* msg_status,
+                         int n_threads) {
+  oracle_w2_decoded d;
+  int rc = oracle_w2_decode(w, ids, id_off, n_keys, &d);
+  if (rc) return rc;
+  mochi_verdicts v = *out;
+  v.grant_valid_bits = NULL;
+  v.grant_flags = NULL;
+  v.grant_ts = NULL;
+  rc = oracle_verify_batch(moduli_be, n_keys, &d.batch, p, &v, n_threads);
+  for (uint32_t i = 0; rc == MOCHI_OK && i < w->n_msgs; i++) {
+    const uint8_t s = d.msg_status[i];
+    if (msg_status) msg_status[i] = s;
+    if (s == MOCHI_MSG_OK) continue;
+    out->cert_accept_bits[i >> 5] &= ~(1u << (i & 31));
+    if (out->cert_reason) out->cert_reason[i] = s == MOCHI_MSG_MALFORMED ? MOCHI_REJECT_MALFORMED : MOCHI_UNDECIDED;
+    if (out->cert_fail_op) out->cert_fail_op[i] = 0xFF;
+  }
+  oracle_w2_free(&d);
+  return rc;
+}

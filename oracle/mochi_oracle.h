@@ -101,6 +101,23 @@ int oracle_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const 
                            const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
                            const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision);
 
+/* Write2ToServer wire decode restated (protobuf-java 3.16.3 semantics, see
+ * mochi_oracle.c) into a mochi_batch whose grant_bytes is the wire blob.
+ * Server ids: key k <-> ids[id_off[k], id_off[k+1]).  Free with oracle_w2_free. */
+typedef struct oracle_w2_decoded {
+  mochi_batch batch;
+  uint8_t* msg_status; /* [M] enum mochi_msg_status */
+} oracle_w2_decoded;
+int oracle_w2_decode(const mochi_write2_batch* w, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids,
+                     oracle_w2_decoded* out);
+void oracle_w2_free(oracle_w2_decoded* d);
+
+/* Decode + oracle_verify_batch + the per-message status fix-up; same contract
+ * as mochi_verify_write2. */
+int oracle_verify_write2(const uint8_t* moduli_be, uint32_t n_keys, const uint8_t* ids, const uint32_t* id_off,
+                         const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* out, uint8_t* msg_status,
+                         int n_threads);
+
 /* --- fixture generation helpers (tests only) --- */
 
 /* Sign SHA-256(msg) with a PEM RSA private key (PKCS#1 v1.5).  Returns 1 ok. */

@@ -43,6 +43,9 @@ def lib():
         L.oracle_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
         L.oracle_write1_uniform.argtypes = [u32, vp, vp]
         L.oracle_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.oracle_w2_decode.argtypes = [vp, vp, vp, u32, vp]
+        L.oracle_w2_free.argtypes = [vp]
+        L.oracle_verify_write2.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, ctypes.c_int]
         L.oracle_rsa_sign.argtypes = [ctypes.c_char_p, vp, sz, vp]
         L.oracle_pem_modulus.argtypes = [ctypes.c_char_p, vp]
         _lib = L
@@ -206,4 +209,66 @@ def write1_classify(requests):
     rc = lib().oracle_write1_classify(len(requests), *[x.ctypes.data for x in a], out.ctypes.data)
     assert rc == 0
     return out[:len(requests)].copy()
+
+
+class W2Decoded_C(ctypes.Structure):
+    pass
+
+
+def _w2_c(wb):
+    import mochi_hip as mh
+
+    return mh.write2_batch_c(wb)
+
+
+def w2_decode(wb, ids, id_off):
+    """Oracle decode of a workload.WireBatch -> dict of numpy arrays (grant_off,
+    grant_len, sig, signer, grant_key, cert_grant_off, cert_op_off, op_key,
+    op_flags, msg_status)."""
+    import mochi_hip as mh
+
+    class Dec(ctypes.Structure):
+        _fields_ = [("batch", mh.Batch_C), ("msg_status", ctypes.POINTER(ctypes.c_uint8))]
+
+    wc, keep = _w2_c(wb)
+    d = Dec()
+    rc = lib().oracle_w2_decode(ctypes.addressof(wc), ids.ctypes.data, id_off.ctypes.data, int(id_off.shape[0]) - 1,
+                                ctypes.addressof(d))
+    assert rc == 0
+    b = d.batch
+    N, C, O = b.n_grants, b.n_certs, b.n_ops
+
+    def arr(ptr, n, dt, shape=None):
+        if n == 0:
+            return np.zeros(shape or (0,), dt)
+        a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
+        a = a.copy()
+        return a.reshape(shape) if shape else a
+
+    out = dict(
+        grant_off=arr(b.grant_off, N, np.uint64), grant_len=arr(b.grant_len, N, np.uint32),
+        sig=arr(b.sig, N * 256, np.uint8, (N, 256)), signer=arr(b.signer, N, np.uint16),
+        grant_key=arr(b.grant_key, N, np.uint8), cert_grant_off=arr(b.cert_grant_off, C + 1, np.uint32),
+        cert_op_off=arr(b.cert_op_off, C + 1, np.uint32), op_key=arr(b.op_key, O, np.uint8),
+        op_flags=arr(b.op_flags, O, np.uint8), msg_status=arr(d.msg_status, C, np.uint8))
+    lib().oracle_w2_free(ctypes.addressof(d))
+    return out
+
+
+def verify_write2(moduli, ids, id_off, wb, replication_factor: int, strict_gt: bool, n_threads: int = 8):
+    import mochi_hip as mh
+
+    mod = np.frombuffer(b"".join(bytes(m) for m in moduli), np.uint8).copy()
+    wc, keep = _w2_c(wb)
+    M = wb.n_msgs
+    out = mh.Verdicts.alloc(0, M)
+    vc = out.to_c()
+    vc.grant_valid_bits = vc.grant_flags = vc.grant_ts = None
+    p = mh.Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+    st = np.zeros(max(M, 1), np.uint8)
+    rc = lib().oracle_verify_write2(mod.ctypes.data, len(moduli), ids.ctypes.data, id_off.ctypes.data,
+                                    ctypes.addressof(wc), ctypes.addressof(p), ctypes.addressof(vc), st.ctypes.data,
+                                    n_threads)
+    assert rc == 0
+    return out, st[:M].copy()
 

@@ -1,0 +1,126 @@
+"""Write2ToServer wire path, CPU side: the oracle's protobuf-java-semantics
+decoder (oracle/mochi_oracle.c) turns the encoded messages back into exactly
+the SoA certificate batch they were built from, and the verdicts through the
+wire equal the verdicts of the SoA batch."""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import workload as W
+
+
+@pytest.fixture(scope="module")
+def pool4():
+    return W.build_pool(R=4, k=1, P=64, P_f=32)
+
+
+@pytest.fixture(scope="module")
+def pool4k2():
+    return W.build_pool(R=4, k=2, P=32, P_f=16)
+
+
+@pytest.mark.parametrize("which", ["k1", "k2"])
+def test_oracle_decode_roundtrip(pool4, pool4k2, which):
+    pool = pool4 if which == "k1" else pool4k2
+    s = W.make_batch(pool, 300, first_cert=41)
+    wb = W.encode_wire_batch(s, pad=3)
+    ids, off = W.server_id_table(4)
+    d = O.w2_decode(wb, ids, off)
+    b = s.batch
+    assert (d["msg_status"] == 0).all()
+    np.testing.assert_array_equal(d["cert_grant_off"], b.cert_grant_off)
+    np.testing.assert_array_equal(d["cert_op_off"], b.cert_op_off)
+    np.testing.assert_array_equal(d["signer"], b.signer)
+    np.testing.assert_array_equal(d["grant_key"], b.grant_key)
+    np.testing.assert_array_equal(d["sig"], b.sig)
+    np.testing.assert_array_equal(d["op_key"], b.op_key)
+    np.testing.assert_array_equal(d["op_flags"], b.op_flags)
+    # grant bytes are wire slices equal to the signed bytes
+    for g in range(0, b.n_grants, 7):
+        a = wb.wire[int(d["grant_off"][g]):int(d["grant_off"][g]) + int(d["grant_len"][g])]
+        e = b.grant_bytes[int(b.grant_off[g]):int(b.grant_off[g]) + int(b.grant_len[g])]
+        np.testing.assert_array_equal(a, e)
+
+
+def test_oracle_wire_verdicts_equal_soa_verdicts(pool4):
+    s = W.make_batch(pool4, 400, first_cert=7)
+    wb = W.encode_wire_batch(s)
+    ids, off = W.server_id_table(4)
+    v, st = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)
+    o = O.verify_batch(pool4.moduli, s.batch, 4, True, 8)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(v.cert_accept_bits, o.cert_accept_bits)
+    np.testing.assert_array_equal(v.cert_reason, o.cert_reason)
+    np.testing.assert_array_equal(v.cert_fail_op, o.cert_fail_op)
+
+
+def _golden():
+    import json
+    import os
+
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "write2_vectors.json")))
+    ids = d["server_ids"]
+    blob = "".join(ids).encode()
+    off = np.zeros(len(ids) + 1, np.uint32)
+    np.cumsum([len(x.encode()) for x in ids], out=off[1:])
+    return d["vectors"], ids, np.frombuffer(blob, np.uint8).copy(), off
+
+
+def _single(data: bytes, n_ops=None):
+    return W.WireBatch(wire=np.frombuffer(data or b"\x00", np.uint8).copy(), msg_off=np.zeros(1, np.uint64),
+                       msg_len=np.array([len(data)], np.uint32), op_flags_off=None, op_flags=np.zeros(1, np.uint8),
+                       expected_hash=np.zeros((1, 128), np.uint8))
+
+
+def check_decode_against_golden(v, d, wire, ids):
+    """Decoded arrays of one golden message vs its pinned status / order / content."""
+    assert int(d["msg_status"][0]) == v["status"], v["name"]
+    if v["status"] != 0:
+        return
+    order, content = v["order"], v["py_content"]
+    assert [o for o in order["ops"]] == content["ops"], v["name"]
+    # op slots: ops naming the same operand1 share a slot
+    exp_slots = [order["ops"].index(k) for k in order["ops"]]
+    got_slots = d["op_key"].tolist()
+    n = len(exp_slots)
+    assert len(got_slots) == n, v["name"]
+    assert all((got_slots[i] == got_slots[j]) == (exp_slots[i] == exp_slots[j]) for i in range(n) for j in range(n)), v["name"]
+    g = 0
+    assert sum(len(x) for x in order["grants"]) == int(d["cert_grant_off"][1]), v["name"]
+    for ci, ckey in enumerate(order["certs"]):
+        c = content["certs"][ckey]
+        sid = c["serverId"]
+        exp_signer = ids.index(sid) if sid in ids else 0xFFFF
+        for gkey in order["grants"][ci]:
+            o, n = int(d["grant_off"][g]), int(d["grant_len"][g])
+            assert wire[o:o + n].hex() == c["grants"][gkey], (v["name"], ckey, gkey)
+            assert int(d["signer"][g]) == exp_signer, v["name"]
+            s = c["sigs"].get(gkey)
+            exp_sig = bytes.fromhex(s) if s is not None and len(s) == 512 else bytes(256)
+            assert d["sig"][g].tobytes() == exp_sig, (v["name"], gkey)
+            exp_key = order["ops"].index(gkey) if gkey in order["ops"] else None
+            if exp_key is None:
+                assert int(d["grant_key"][g]) == 0xFF, v["name"]
+            else:
+                assert int(d["grant_key"][g]) == got_slots[exp_key], v["name"]
+            g += 1
+
+
+def test_oracle_decode_matches_golden_vectors():
+    vecs, ids, blob, off = _golden()
+    assert len(vecs) >= 50
+    for v in vecs:
+        data = bytes.fromhex(v["hex"])
+        d = O.w2_decode(_single(data), blob, off)
+        check_decode_against_golden(v, d, data, ids)
+
+
+def test_oracle_ops_mismatch_status():
+    vecs, ids, blob, off = _golden()
+    v = next(x for x in vecs if x["name"] == "canonical")
+    data = bytes.fromhex(v["hex"])
+    wb = _single(data)
+    wb.op_flags_off = np.array([0, 3], np.uint32)  # message holds 2 ops
+    wb.op_flags = np.full(3, 3, np.uint8)
+    d = O.w2_decode(wb, blob, off)
+    assert int(d["msg_status"][0]) == 3

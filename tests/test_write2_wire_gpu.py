@@ -1,0 +1,185 @@
+"""Write2ToServer wire path on the GPU (mochi_verify_write2 / mochi_write2_decode):
+the device decoder agrees with the oracle decoder array for array, with the
+golden protobuf vectors, and the wire path's verdicts equal the SoA path's."""
+import numpy as np
+import pytest
+
+import mochi_hip as mh
+import oracle_ffi as O
+import workload as W
+from test_write2_wire_cpu import _golden, check_decode_against_golden
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off", "cert_op_off", "op_key",
+        "op_flags", "msg_status")
+
+
+@pytest.fixture(scope="module")
+def pool4():
+    return W.build_pool(R=4, k=1, P=512, P_f=64)
+
+
+@pytest.fixture(scope="module")
+def pool7k2():
+    return W.build_pool(R=7, k=2, P=256, P_f=64)
+
+
+def _ver(pool):
+    v = mh.Verifier(pool.moduli, 0)
+    v.set_server_ids(W.SERVER_IDS[:pool.R])
+    return v
+
+
+def _pack(msgs, pad=1):
+    off, parts, pos = [], [], 0
+    for i, m in enumerate(msgs):
+        p = (i * pad) % 4
+        parts.append(b"\x00" * p)
+        pos += p
+        off.append(pos)
+        parts.append(m)
+        pos += len(m)
+    M = len(msgs)
+    return W.WireBatch(wire=np.frombuffer(b"".join(parts) or b"\x00", np.uint8).copy(),
+                       msg_off=np.array(off, np.uint64), msg_len=np.array([len(m) for m in msgs], np.uint32),
+                       op_flags_off=None, op_flags=np.zeros(1, np.uint8),
+                       expected_hash=np.zeros((M, 128), np.uint8))
+
+
+def assert_decode_equal(a, b, what=""):
+    for k in KEYS:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} {what}")
+
+
+def test_device_decode_golden_vectors(pool4):
+    vecs, ids, blob, off = _golden()
+    ver = mh.Verifier(pool4.moduli[:1] * len(ids), 0)
+    ver.set_server_ids(ids)
+    msgs = [bytes.fromhex(v["hex"]) for v in vecs]
+    wb = _pack(msgs)
+    d = ver.decode_write2(wb)
+    o = O.w2_decode(wb, blob, off)
+    assert_decode_equal(d, o, "golden batch")
+    # and each vector on its own against its pinned expectations
+    for v, m in zip(vecs, msgs):
+        one = _pack([m])
+        dd = ver.decode_write2(one)
+        check_decode_against_golden(v, dd, m, ids)
+    ver.close()
+
+
+@pytest.mark.parametrize("strict", [True, False])
+def test_wire_verdicts_equal_soa_verdicts(pool4, strict):
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 3000, first_cert=321)
+    wb = W.encode_wire_batch(s, pad=5)
+    g, st = ver.verify_write2(wb, 4, strict)
+    assert (st == 0).all()
+    soa = ver.verify(s.batch, 4, strict)
+    np.testing.assert_array_equal(g.cert_accept_bits, soa.cert_accept_bits)
+    np.testing.assert_array_equal(g.cert_reason, soa.cert_reason)
+    np.testing.assert_array_equal(g.cert_fail_op, soa.cert_fail_op)
+    ids, off = W.server_id_table(4)
+    o, ost = O.verify_write2(pool4.moduli, ids, off, wb, 4, strict)
+    np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits)
+    np.testing.assert_array_equal(g.cert_reason, o.cert_reason)
+    np.testing.assert_array_equal(st, ost)
+    d = ver.decode_write2(wb)
+    np.testing.assert_array_equal(d["signer"], s.batch.signer)
+    np.testing.assert_array_equal(d["sig"], s.batch.sig)
+    ver.close()
+
+
+def test_wire_r7_k2(pool7k2):
+    ver = _ver(pool7k2)
+    s = W.make_batch(pool7k2, 1500, first_cert=11)
+    wb = W.encode_wire_batch(s)
+    for strict in (True, False):
+        g, st = ver.verify_write2(wb, 7, strict)
+        soa = ver.verify(s.batch, 7, strict)
+        np.testing.assert_array_equal(g.cert_reason, soa.cert_reason)
+        np.testing.assert_array_equal(g.cert_accept_bits, soa.cert_accept_bits)
+    ver.close()
+
+
+def _mutate(rng, s, c, ids):
+    """One certificate's message with a structural mutation (decode-semantics fuzz)."""
+    b = s.batch
+    g0, g1 = int(b.cert_grant_off[c]), int(b.cert_grant_off[c + 1])
+    mgs = {}
+    for g in range(g0, g1):
+        gb = b.grant_bytes[int(b.grant_off[g]):int(b.grant_off[g]) + int(b.grant_len[g])].tobytes()
+        mgs.setdefault(int(b.signer[g]), []).append((W.grant_object_id(gb), gb, b.sig[g].tobytes()))
+    order = list(mgs)
+    kind = int(rng.integers(0, 9))
+    if kind == 1:
+        rng.shuffle(order)  # MultiGrant wire order decides g0
+    enc = []
+    for r in order:
+        items = mgs[r]
+        sigs = [(o, sg) for o, _, sg in items]
+        if kind == 2:
+            sigs = sigs[1:]  # a grant without signature
+        extra = b""
+        if kind == 3:
+            extra = b"\x48\x07" + W._ld(13, b"unknown")  # unknown fields
+        enc.append((ids[r], W.encode_multigrant([(o, gb) for o, gb, _ in items], ids[r], "cl", "", sigs) + extra))
+    if kind == 4 and len(enc) > 1:
+        enc.append((enc[0][0], enc[-1][1]))  # repeated certificate key: first place, last value
+    if kind == 5:
+        enc.insert(0, (ids[order[0]], enc[0][1]))  # duplicate of the first entry
+    ops = [W.encode_operation(2, o) for o, _, _ in mgs[order[0]]]
+    if kind == 6:
+        ops = ops + ops  # ops repeating a key (multiplicity)
+    m = W.encode_write2(enc, ops)
+    if kind == 7 and len(m) > 8:
+        i = int(rng.integers(0, len(m)))
+        m = m[:i] + bytes([m[i] ^ (1 << int(rng.integers(0, 8)))]) + m[i + 1:]  # random bit flip
+    if kind == 8:
+        m = m[:int(rng.integers(0, len(m) + 1))]  # truncation
+    return m
+
+
+def test_wire_fuzz_device_equals_oracle(pool4):
+    ver = _ver(pool4)
+    rng = np.random.default_rng(2024)
+    s = W.make_batch(pool4, 2000, first_cert=999)
+    msgs = [_mutate(rng, s, c, W.SERVER_IDS) for c in range(s.batch.n_certs)]
+    wb = _pack(msgs, pad=3)
+    wb.expected_hash = s.batch.expected_hash.copy()
+    ids, off = W.server_id_table(4)
+    d = ver.decode_write2(wb)
+    o = O.w2_decode(wb, ids, off)
+    assert_decode_equal(d, o, "fuzz")
+    assert len(set(d["msg_status"].tolist())) >= 2
+    for strict in (True, False):
+        g, st = ver.verify_write2(wb, 4, strict)
+        ov, ost = O.verify_write2(pool4.moduli, ids, off, wb, 4, strict)
+        np.testing.assert_array_equal(st, ost)
+        np.testing.assert_array_equal(g.cert_reason, ov.cert_reason)
+        np.testing.assert_array_equal(g.cert_fail_op, ov.cert_fail_op)
+        np.testing.assert_array_equal(g.cert_accept_bits, ov.cert_accept_bits)
+    ver.close()
+
+
+def test_wire_edge_shapes(pool4):
+    ver = _ver(pool4)
+    # no messages
+    g, st = ver.verify_write2(_pack([]), 4, True)
+    assert st.size == 0
+    # op_flags CSR disagreeing with the message -> OPS_MISMATCH / UNDECIDED
+    s = W.make_batch(pool4, 40, faults=False)
+    wb = W.encode_wire_batch(s)
+    wb.op_flags_off = wb.op_flags_off.copy()
+    wb.op_flags_off[5:] += 1
+    wb.op_flags = np.concatenate([wb.op_flags, np.full(1, 3, np.uint8)])
+    g, st = ver.verify_write2(wb, 4, True)
+    assert st[4] == mh.MSG_OPS_MISMATCH and g.cert_reason[4] == mh.UNDECIDED and not g.cert_accept[4]
+    assert (st[:4] == 0).all() and (st[5:] == 0).all()
+    # op_flags from the caller: a non-local op is WRONG_SHARD, never checked
+    wb2 = W.encode_wire_batch(s)
+    wb2.op_flags[:] = 0
+    g2, st2 = ver.verify_write2(wb2, 4, True)
+    assert g2.cert_accept.all()
+    ver.close()
