@@ -53,6 +53,7 @@ def parse_args():
     ap.add_argument("--pool", type=int, default=4096, help="unique signed grant templates per server")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wire", action="store_true", help="skip the Write2ToServer wire-path measurement")
     ap.add_argument("--cache-dir", default=os.environ.get("MOCHI_CACHE", "/tmp/mochi_bench_cache"))
     return ap.parse_args()
 
@@ -166,6 +167,7 @@ def main():
                                           np.array_equal(z["cert_reason"], host.cert_reason[:z["cert_reason"].shape[0]]))
         # PCIe-inclusive host path (never the headline value)
         host = host_path(ver, batch, R, strict)
+        wire = None if args.no_wire else wire_path(ver, pool, synth, R, strict, local_rank, stream, args)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -206,6 +208,7 @@ def main():
                          "tally": round(stage_ms[4], 4)},
             "host_path_pcie_inclusive_grants_per_s": host["pinned_grants_per_s"],
             "host_path": host,
+            "write2_wire_path": wire,
             "correct_vs_ground_truth": all_ok,
             "cpu_baseline": cpu,
             "wall_s": round(wall_max, 4),
@@ -238,6 +241,46 @@ def host_path(ver, batch, R, strict, reps=3):
         out[f"{name}_wall_grants_per_s"] = round(N / best_wall, 1)
     out["note"] = "chunked pipeline, 262144-grant chunks; device-event span unless *_wall_*"
     return out
+
+
+def wire_path(ver, pool, synth, R, strict, dev, stream, args):
+    """Device-resident Write2ToServer wire messages -> verdicts (mochi_verify_write2_device):
+    the device protobuf decode (k_w2_count + scans + k_w2_emit) + the same verify
+    path + status fix-up, timed like the headline (events around K calls).
+    Reported beside the headline; the headline stays the SoA batch path."""
+    import numpy as np
+    import torch
+
+    import mochi_hip as mh
+    import workload as W
+
+    t0 = time.perf_counter()
+    wb = W.encode_wire_batch(synth)
+    enc_s = time.perf_counter() - t0
+    ver.set_server_ids(W.SERVER_IDS[:R])
+    dwb = mh.DeviceWireBatch(wb, dev)
+    out = mh.DeviceVerdicts(0, wb.n_msgs, dev, full=True)
+    out.grant_flags = out.grant_ts = None
+    for _ in range(max(1, args.warmup)):
+        ver.verify_write2_device(dwb, out, R, strict, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    host = out.to_host()
+    ref = ver.verify(synth.batch, R, strict)
+    same = bool(np.array_equal(host.cert_reason, ref.cert_reason) and
+                np.array_equal(host.cert_accept_bits, ref.cert_accept_bits) and
+                int(dwb.status.max().item()) == 0)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        ver.verify_write2_device(dwb, out, R, strict, stream=stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / args.steps
+    N = synth.batch.n_grants
+    return {"grants_per_s": round(N / t, 1), "ms_per_step": round(t * 1e3, 4), "messages": wb.n_msgs,
+            "wire_bytes": int(wb.wire.nbytes), "verdicts_equal_soa_path": same,
+            "host_encode_s": round(enc_s, 2),
+            "note": "Write2ToServer bodies resident in HBM; includes one host wait on the decoded totals per step"}
 
 
 def run_cpu_baseline(args, R, k, flags_out):

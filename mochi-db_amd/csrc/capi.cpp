@@ -175,7 +175,7 @@ struct mochi_ctx {
   DevBuf ids, id_off;
   uint32_t n_ids = 0;
   DevBuf w2_cnt_g, w2_cnt_o, w2_status, w2_scan, w2_cg, w2_co, w2_goff, w2_glen, w2_sig, w2_signer, w2_gkey,
-      w2_okey, w2_oflags;
+      w2_okey, w2_oflags, w2_sigsrc;
   PinnedBuf w2_tot;
   // per-stage profiling (mochi_ctx_set_profiling): one event set per verify call
   bool profiling = false;
@@ -633,8 +633,11 @@ int run_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_par
   const uint32_t N = tot[0], O = tot[1];
   if ((rc = c->w2_goff.ensure(8 * (size_t)N)) || (rc = c->w2_glen.ensure(4 * (size_t)N)) ||
       (rc = c->w2_sig.ensure((size_t)MOCHI_RSA_BYTES * N)) || (rc = c->w2_signer.ensure(2 * (size_t)N)) ||
-      (rc = c->w2_gkey.ensure(N)) || (rc = c->w2_okey.ensure(O)) || (rc = c->w2_oflags.ensure(O)))
+      (rc = c->w2_gkey.ensure(N)) || (rc = c->w2_okey.ensure(O)) || (rc = c->w2_oflags.ensure(O)) ||
+      (rc = c->w2_sigsrc.ensure(8 * (size_t)N)))
     return rc;
+  a.N = N;
+  a.sig_src = c->w2_sigsrc.as<uint64_t>();
   a.grant_off = c->w2_goff.as<uint64_t>();
   a.grant_len = c->w2_glen.as<uint32_t>();
   a.sig = c->w2_sig.as<uint8_t>();

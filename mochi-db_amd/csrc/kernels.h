@@ -75,6 +75,8 @@ struct W2Args {
   size_t scan_temp_bytes;
   uint32_t* cert_grant_off;  // [M+1]
   uint32_t* cert_op_off;     // [M+1]
+  uint32_t N;          // decoded grant total (emit)
+  uint64_t* sig_src;   // [N] wire offset of each signature (emit -> k_w2_sig)
   uint64_t* grant_off;
   uint32_t* grant_len;
   uint8_t* sig;

@@ -67,6 +67,16 @@ __device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
   uint32_t i = 0;
 #pragma unroll 1
   while (i < n) {
+    // 16 ASCII bytes per step once the position is 16-byte aligned (all 16
+    // bytes lie inside the string, so the load stays in bounds)
+    const uintptr_t addr = r.abase + (uintptr_t)(off + i + r.shift);
+    if ((addr & 15) == 0 && i + 16 <= n) {
+      const uint4 v = *(const uint4*)addr;
+      if (((v.x | v.y | v.z | v.w) & 0x80808080u) == 0) {
+        i += 16;
+        continue;
+      }
+    }
     const uint32_t c = r.at(off + i);
     if (c < 0x80) {
       // ASCII fast path: skip every remaining byte of the cached word when all

@@ -70,7 +70,8 @@ __device__ __forceinline__ bool vlen(ByteReader& r, uint32_t& pos, uint32_t end,
 }
 
 // Skip an unknown group opened by `field` (skipMessage + checkLastTagWas).
-__device__ bool skip_group(ByteReader& r, uint32_t& pos, uint32_t end, uint32_t field) {
+// Rare: kept out of line so its stack does not weigh on the common path.
+__device__ __noinline__ bool skip_group(ByteReader& r, uint32_t& pos, uint32_t end, uint32_t field) {
   uint32_t stack[kMaxGroupDepth];
   int depth = 1;
   stack[0] = field;
@@ -388,6 +389,7 @@ __device__ bool grant_canonical(ByteReader& r, uint32_t off, uint32_t len) {
 // Decode one valid message.  COUNT: returns status and counts.  EMIT: writes
 // outputs at g_base / o_base.  Mirrors oracle/mochi_oracle.c decode_one.
 struct W2Out {
+  uint64_t* sig_src;  // wire offset of each grant's 256-byte signature, ~0 = none
   uint64_t* grant_off;
   uint32_t* grant_len;
   uint8_t* sig;
@@ -500,16 +502,8 @@ __device__ uint32_t decode_msg(ByteReader& r, uint64_t msg_off, const uint8_t* _
           }
         }
       }
-      uint4* dst = (uint4*)(out.sig + (size_t)g * MOCHI_RSA_BYTES);
-      if (have && s_len == MOCHI_RSA_BYTES) {
-#pragma unroll 4
-        for (int q = 0; q < 16; q++)
-          dst[q] = make_uint4(ld4(r.base, s_off + 16 * q), ld4(r.base, s_off + 16 * q + 4),
-                              ld4(r.base, s_off + 16 * q + 8), ld4(r.base, s_off + 16 * q + 12));
-      } else {
-#pragma unroll 4
-        for (int q = 0; q < 16; q++) dst[q] = make_uint4(0, 0, 0, 0);
-      }
+      // the 256 signature bytes are gathered by k_w2_sig (coalesced, 16 lanes per grant)
+      out.sig_src[g] = have && s_len == MOCHI_RSA_BYTES ? msg_off + s_off : ~0ull;
       // key slot of the first op naming this grant's key
       uint8_t key = 0xFF;
       {
@@ -581,6 +575,28 @@ __global__ __launch_bounds__(256) void k_w2_emit(const uint8_t* __restrict__ wir
                    flags_off ? flags_in + flags_off[m] : nullptr, out);
 }
 
+// sig[g] = wire[sig_src[g] .. +256) (zeros when absent): 16 lanes per grant,
+// each moving 16 bytes, so a wave reads 4 signatures' contiguous bytes.
+__global__ __launch_bounds__(256) void k_w2_sig(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ sig_src,
+                                                uint32_t N, uint8_t* __restrict__ sig) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = (uint32_t)(t >> 4), q = (uint32_t)(t & 15);
+  if (g >= N) return;
+  const uint64_t src = sig_src[g];
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (src != ~0ull) {
+    const uint8_t* p = wire + src + 16 * q;
+    const uintptr_t a = (uintptr_t)p;
+    if ((a & 3) == 0) {
+      const uint32_t* w = (const uint32_t*)p;
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      v = make_uint4(ld4(p, 0), ld4(p, 4), ld4(p, 8), ld4(p, 12));
+    }
+  }
+  ((uint4*)(sig + (size_t)g * MOCHI_RSA_BYTES))[q] = v;
+}
+
 __global__ __launch_bounds__(256) void k_w2_fixup(const uint8_t* __restrict__ status, uint32_t M,
                                                   uint32_t* __restrict__ accept_bits, uint8_t* __restrict__ reason,
                                                   uint8_t* __restrict__ fail_op) {
@@ -620,10 +636,11 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
 }
 
 hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
-  W2Out o{a.grant_off, a.grant_len, a.sig, a.signer, a.grant_key, a.op_key, a.op_flags};
+  W2Out o{a.sig_src, a.grant_off, a.grant_len, a.sig, a.signer, a.grant_key, a.op_key, a.op_flags};
   if (a.M)
     hipLaunchKernelGGL(k_w2_emit, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, a.ids,
                        a.id_off, a.n_ids, a.flags_off, a.flags_in, a.cert_grant_off, a.cert_op_off, a.status, o);
+  if (a.N) hipLaunchKernelGGL(k_w2_sig, dim3(cdiv((uint64_t)a.N * 16, 256)), dim3(256), 0, st, a.wire, a.sig_src, a.N, a.sig);
   return hipGetLastError();
 }
 

@@ -369,6 +369,19 @@ class Verifier:
         out.timing_ms = {"total": t.value}
         return out, st[:M].copy()
 
+    def verify_write2_device(self, dwb: "DeviceWireBatch", out: "DeviceVerdicts", replication_factor: int,
+                             strict_gt: bool = True, stream: int = 0) -> None:
+        """Device-resident Write2 wire messages -> certificate verdicts (async on `stream`,
+        except for one wait on the decoded grant / op totals)."""
+        wc = dwb.to_c()
+        vc = out.to_c()
+        vc.grant_valid_bits = vc.grant_flags = vc.grant_ts = None
+        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        rc = self.lib.mochi_verify_write2_device(self.ctx, ctypes.addressof(wc), ctypes.addressof(p),
+                                                 ctypes.addressof(vc), dwb.status.data_ptr(), stream)
+        if rc != OK:
+            raise MochiError(f"mochi_verify_write2_device rc={rc}: {_err(self.lib)}")
+
     def decode_write2(self, wb) -> dict:
         """The device decoder's SoA view of the messages (inspection / tests)."""
         wc, keep = write2_batch_c(wb)
@@ -490,27 +503,6 @@ class DeviceBatch:
         self.op_flags = t(b.op_flags)
         self.expected_hash = t(b.expected_hash)
 
-    def pinned(self) -> "Batch":
-        """A copy whose arrays live in one pinned host allocation (mochi_host_alloc):
-        mochi_verify_batch DMAs such arrays in place instead of staging them."""
-        b = self.normalized()
-        names = ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off",
-                 "cert_op_off", "op_key", "op_flags", "expected_hash")
-        arrs = [getattr(b, nm) for nm in names]
-        offs, total = [], 0
-        for a in arrs:
-            offs.append(total)
-            total = (total + a.nbytes + 255) // 256 * 256
-        buf = PinnedHost(total)
-        out = {}
-        for nm, a, o in zip(names, arrs, offs):
-            v = np.frombuffer(buf.view()[o:o + a.nbytes], dtype=a.dtype).reshape(a.shape)
-            v[...] = a
-            out[nm] = v
-        pb = Batch(**out)
-        pb._pinned = buf  # keep the allocation alive with the views
-        return pb
-
     def to_c(self) -> Batch_C:
         b = Batch_C()
         b.n_grants, b.n_certs, b.n_ops = self.n_grants, self.n_certs, self.n_ops
@@ -519,6 +511,33 @@ class DeviceBatch:
                      "cert_op_off", "op_key", "op_flags", "expected_hash"):
             setattr(b, name, getattr(self, name).data_ptr())
         return b
+
+
+class DeviceWireBatch:
+    """A workload.WireBatch copied into device memory with torch (plumbing only)."""
+
+    def __init__(self, wb, device: int = 0):
+        import torch
+
+        dev = torch.device("cuda", device)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.n_msgs = wb.n_msgs
+        self.wire = t(wb.wire)
+        self.msg_off = t(np.ascontiguousarray(wb.msg_off, np.uint64).view(np.int64))
+        self.msg_len = t(np.ascontiguousarray(wb.msg_len, np.uint32).view(np.int32))
+        self.op_flags_off = None if wb.op_flags_off is None else t(np.ascontiguousarray(wb.op_flags_off, np.uint32).view(np.int32))
+        self.op_flags = t(wb.op_flags if wb.op_flags.size else np.zeros(1, np.uint8))
+        self.expected_hash = t(np.ascontiguousarray(wb.expected_hash, np.uint8).reshape(-1))
+        self.status = torch.zeros(max(self.n_msgs, 1), dtype=torch.uint8, device=dev)
+
+    def to_c(self) -> "Write2Batch_C":
+        c = Write2Batch_C()
+        c.n_msgs = self.n_msgs
+        c.wire_len = int(self.wire.numel())
+        c.wire, c.msg_off, c.msg_len = self.wire.data_ptr(), self.msg_off.data_ptr(), self.msg_len.data_ptr()
+        c.op_flags_off = None if self.op_flags_off is None else self.op_flags_off.data_ptr()
+        c.op_flags, c.expected_hash = self.op_flags.data_ptr(), self.expected_hash.data_ptr()
+        return c
 
 
 class DeviceVerdicts:
