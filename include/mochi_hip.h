@@ -364,6 +364,35 @@ typedef struct mochi_write2_decoded {
 int mochi_write2_decode(mochi_ctx* ctx, const mochi_write2_batch* batch, mochi_write2_decoded* out);
 void mochi_write2_decoded_free(mochi_write2_decoded* d);
 
+/* ------------------------------------------------------------------------
+ * Micro-batcher: the blocking per-request call the Java handler keeps
+ * (Write2ToServerRequestHandler.handle -> processWrite2ToServer on a 2..20
+ * thread pool, MochiServer.java:36-40), coalesced across threads into one
+ * mochi_verify_write2 call by a flusher thread: a batch goes out when
+ * max_msgs requests are pending or the oldest has waited max_wait_us.
+ * ------------------------------------------------------------------------ */
+typedef struct mochi_batcher mochi_batcher;
+
+typedef struct mochi_verdict1 {
+  uint8_t accepted;   /* certificate accepted                 */
+  uint8_t reason;     /* enum mochi_reason                    */
+  uint8_t fail_op;    /* first failing op, 0xFF if none       */
+  uint8_t msg_status; /* enum mochi_msg_status                */
+} mochi_verdict1;
+
+/* with_op_flags: 1 = every call passes op_flags[n_ops] (MOCHI_OP_* per op, in
+ * transaction order); 0 = calls pass NULL / 0 and every op counts as
+ * LOCAL|HAS_SVOC.  The batcher borrows `ctx` (one batcher per context). */
+mochi_batcher* mochi_batcher_create(mochi_ctx* ctx, const mochi_params* params, uint32_t max_msgs,
+                                    uint32_t max_wait_us, int with_op_flags);
+/* Blocks until this message's verdict is in `out`.  Thread-safe.  Returns the
+ * status of the batch call that carried it. */
+int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
+                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict1* out);
+int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs);
+/* Drains pending requests, then stops the flusher. */
+void mochi_batcher_destroy(mochi_batcher* b);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,200 @@
+// batcher.cpp — the micro-batcher in front of mochi_verify_write2.
+//
+// The reference validates one Write2ToServer per worker-thread call
+// (Write2ToServerRequestHandler.handle -> InMemoryDataStore.processWrite2ToServer,
+// Write2ToServerRequestHandler.java:25-31, InMemoryDataStore.java:641-666) on a
+// ThreadPoolExecutor of core 2 / max 20 threads (MochiServer.java:36-40).  One
+// certificate is far too little work for a GPU launch, so the drop-in keeps
+// that blocking per-request call and coalesces the requests of all threads:
+// callers enqueue their message and sleep; one flusher thread takes up to
+// max_msgs pending messages (or whatever is pending once the oldest has waited
+// max_wait_us), verifies them with ONE mochi_verify_write2 call, and wakes each
+// caller with its own verdict.  While a batch is on the GPU the next one
+// accumulates, so the batch size follows the offered load.
+//
+// Built only on the public C ABI (include/mochi_hip.h).
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/mochi_hip.h"
+
+namespace {
+
+struct Request {
+  const uint8_t* msg;
+  uint32_t msg_len;
+  const uint8_t* op_flags;  // may be null (every op LOCAL|HAS_SVOC)
+  uint32_t n_ops;
+  const uint8_t* expected_hash;
+  std::chrono::steady_clock::time_point t_enq;
+  mochi_verdict1* out;
+  int rc = 0;
+  bool done = false;
+};
+
+}  // namespace
+
+struct mochi_batcher {
+  mochi_ctx* ctx;
+  mochi_params params;
+  uint32_t max_msgs, max_wait_us;
+  bool with_op_flags;
+  std::mutex mu;
+  std::condition_variable cv_work, cv_done;
+  std::deque<Request*> q;
+  bool stop = false;
+  uint64_t n_batches = 0, n_msgs = 0;
+  std::thread flusher;
+  // batch assembly buffers (flusher thread only)
+  std::vector<uint8_t> wire, flags, hashes, status, reason, fail_op;
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> len, flags_off, accept;
+
+  void run() {
+    std::vector<Request*> batch;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_work.wait(lk, [&] { return stop || !q.empty(); });
+        if (q.empty() && stop) return;
+        // wait for a full batch or for the oldest request's deadline
+        const auto deadline = q.front()->t_enq + std::chrono::microseconds(max_wait_us);
+        cv_work.wait_until(lk, deadline, [&] { return stop || q.size() >= max_msgs; });
+        const size_t n = q.size() < max_msgs ? q.size() : max_msgs;
+        batch.assign(q.begin(), q.begin() + n);
+        q.erase(q.begin(), q.begin() + n);
+      }
+      verify(batch);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        for (Request* r : batch) r->done = true;
+        n_batches++;
+        n_msgs += batch.size();
+      }
+      cv_done.notify_all();
+    }
+  }
+
+  void verify(const std::vector<Request*>& batch) {
+    const uint32_t M = (uint32_t)batch.size();
+    size_t total = 0, n_ops = 0;
+    const bool any_flags = with_op_flags;
+    for (Request* r : batch) {
+      total += r->msg_len;
+      n_ops += r->n_ops;
+    }
+    wire.resize(total ? total : 1);
+    off.resize(M);
+    len.resize(M);
+    hashes.resize((size_t)M * MOCHI_TXN_HASH_BYTES);
+    flags_off.resize(M + 1);
+    flags.resize(n_ops ? n_ops : 1);
+    size_t pos = 0, op = 0;
+    for (uint32_t i = 0; i < M; i++) {
+      Request* r = batch[i];
+      memcpy(wire.data() + pos, r->msg, r->msg_len);
+      off[i] = pos;
+      len[i] = r->msg_len;
+      pos += r->msg_len;
+      memcpy(hashes.data() + (size_t)i * MOCHI_TXN_HASH_BYTES, r->expected_hash, MOCHI_TXN_HASH_BYTES);
+      flags_off[i] = (uint32_t)op;
+      for (uint32_t j = 0; j < r->n_ops; j++)
+        flags[op + j] = r->op_flags ? r->op_flags[j] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
+      op += r->n_ops;
+    }
+    flags_off[M] = (uint32_t)op;
+    mochi_write2_batch w;
+    memset(&w, 0, sizeof w);
+    w.n_msgs = M;
+    w.wire_len = total;
+    w.wire = wire.data();
+    w.msg_off = off.data();
+    w.msg_len = len.data();
+    // without per-op flags the decoder's default (LOCAL|HAS_SVOC) applies
+    w.op_flags_off = any_flags ? flags_off.data() : nullptr;
+    w.op_flags = any_flags ? flags.data() : nullptr;
+    w.expected_hash = hashes.data();
+    accept.assign((M + 31) / 32, 0);
+    reason.resize(M);
+    fail_op.resize(M);
+    status.resize(M);
+    mochi_verdicts v;
+    memset(&v, 0, sizeof v);
+    v.cert_accept_bits = accept.data();
+    v.cert_reason = reason.data();
+    v.cert_fail_op = fail_op.data();
+    const int rc = mochi_verify_write2(ctx, &w, &params, &v, status.data());
+    for (uint32_t i = 0; i < M; i++) {
+      Request* r = batch[i];
+      r->rc = rc;
+      if (rc == MOCHI_OK) {
+        r->out->accepted = (uint8_t)((accept[i >> 5] >> (i & 31)) & 1u);
+        r->out->reason = reason[i];
+        r->out->fail_op = fail_op[i];
+        r->out->msg_status = status[i];
+      }
+    }
+  }
+};
+
+extern "C" {
+
+mochi_batcher* mochi_batcher_create(mochi_ctx* ctx, const mochi_params* params, uint32_t max_msgs,
+                                    uint32_t max_wait_us, int with_op_flags) {
+  if (!ctx || !params || max_msgs == 0) return nullptr;
+  mochi_batcher* b = new mochi_batcher();
+  b->with_op_flags = with_op_flags != 0;
+  b->ctx = ctx;
+  b->params = *params;
+  b->max_msgs = max_msgs;
+  b->max_wait_us = max_wait_us;
+  b->flusher = std::thread([b] { b->run(); });
+  return b;
+}
+
+int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
+                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict1* out) {
+  if (!b || (!msg && msg_len) || !expected_hash || !out) return MOCHI_EINVAL;
+  if (b->with_op_flags ? (op_flags == nullptr && n_ops != 0) : (op_flags != nullptr || n_ops != 0))
+    return MOCHI_EINVAL;
+  Request r;
+  r.msg = msg;
+  r.msg_len = msg_len;
+  r.op_flags = op_flags;
+  r.n_ops = n_ops;
+  r.expected_hash = expected_hash;
+  r.out = out;
+  r.t_enq = std::chrono::steady_clock::now();
+  std::unique_lock<std::mutex> lk(b->mu);
+  if (b->stop) return MOCHI_EINVAL;
+  b->q.push_back(&r);
+  if (b->q.size() == 1 || b->q.size() >= b->max_msgs) b->cv_work.notify_one();
+  b->cv_done.wait(lk, [&] { return r.done; });
+  return r.rc;
+}
+
+int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs) {
+  if (!b) return MOCHI_EINVAL;
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (batches) *batches = b->n_batches;
+  if (msgs) *msgs = b->n_msgs;
+  return MOCHI_OK;
+}
+
+void mochi_batcher_destroy(mochi_batcher* b) {
+  if (!b) return;
+  {
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->stop = true;
+  }
+  b->cv_work.notify_all();
+  if (b->flusher.joinable()) b->flusher.join();
+  delete b;
+}
+
+}  // extern "C"

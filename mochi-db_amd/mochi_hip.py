@@ -146,6 +146,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_verify_write2_device.argtypes = [vp, vp, vp, vp, vp, vp]
     lib.mochi_write2_decode.argtypes = [vp, vp, vp]
     lib.mochi_write2_decoded_free.argtypes = [vp]
+    lib.mochi_batcher_create.restype = vp
+    lib.mochi_batcher_create.argtypes = [vp, vp, u32, u32, ctypes.c_int]
+    lib.mochi_batcher_verify.argtypes = [vp, vp, u32, vp, u32, vp, vp]
+    lib.mochi_batcher_stats.argtypes = [vp, vp, vp]
+    lib.mochi_batcher_destroy.argtypes = [vp]
     lib.mochi_host_alloc.restype = vp
     lib.mochi_host_alloc.argtypes = [ctypes.c_uint64]
     lib.mochi_host_free.argtypes = [vp]
@@ -711,4 +716,44 @@ class Write2Decoded_C(ctypes.Structure):
                 ("sig", ctypes.c_void_p), ("signer", ctypes.c_void_p), ("grant_key", ctypes.c_void_p),
                 ("cert_grant_off", ctypes.c_void_p), ("cert_op_off", ctypes.c_void_p), ("op_key", ctypes.c_void_p),
                 ("op_flags", ctypes.c_void_p), ("msg_status", ctypes.c_void_p)]
+
+
+class Verdict1_C(ctypes.Structure):
+    _fields_ = [("accepted", ctypes.c_uint8), ("reason", ctypes.c_uint8), ("fail_op", ctypes.c_uint8),
+                ("msg_status", ctypes.c_uint8)]
+
+
+class Batcher:
+    """mochi_batcher: blocking per-request verify, coalesced across calling threads.
+    (ctypes drops the GIL during the call, so Python threads block concurrently.)"""
+
+    def __init__(self, verifier: "Verifier", replication_factor: int, strict_gt: bool = True, max_msgs: int = 4096,
+                 max_wait_us: int = 200, with_op_flags: bool = False):
+        self.lib = verifier.lib
+        self._ver = verifier
+        self._p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        self.with_op_flags = with_op_flags
+        self.h = self.lib.mochi_batcher_create(verifier.ctx, ctypes.addressof(self._p), max_msgs, max_wait_us,
+                                               1 if with_op_flags else 0)
+        if not self.h:
+            raise MochiError("mochi_batcher_create failed")
+
+    def verify(self, msg: bytes, expected_hash: bytes, op_flags: Optional[bytes] = None):
+        out = Verdict1_C()
+        fl = op_flags if op_flags is not None else None
+        rc = self.lib.mochi_batcher_verify(self.h, msg, len(msg), fl, len(fl) if fl else 0, expected_hash,
+                                           ctypes.byref(out))
+        if rc != OK:
+            raise MochiError(f"mochi_batcher_verify rc={rc}: {_err(self.lib)}")
+        return bool(out.accepted), out.reason, out.fail_op, out.msg_status
+
+    def stats(self):
+        b, m = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.mochi_batcher_stats(self.h, ctypes.byref(b), ctypes.byref(m))
+        return b.value, m.value
+
+    def close(self):
+        if self.h:
+            self.lib.mochi_batcher_destroy(self.h)
+            self.h = None
 

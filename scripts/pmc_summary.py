@@ -30,8 +30,17 @@ def load_pass(name):
     if not files:
         return {}
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for r in csv.DictReader(open(files[0])):
+    rows = list(csv.DictReader(open(files[0])))
+    # only the headline dispatches: per kernel, the largest grid (bench.py also
+    # runs host-path chunks and the wire path, which launch smaller grids)
+    big = collections.defaultdict(int)
+    for r in rows:
         k = r["Kernel_Name"].split("(")[0].replace("mochi::", "")
+        big[k] = max(big[k], int(r["Grid_Size"]))
+    for r in rows:
+        k = r["Kernel_Name"].split("(")[0].replace("mochi::", "")
+        if int(r["Grid_Size"]) != big[k]:
+            continue
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 

@@ -183,3 +183,43 @@ def test_wire_edge_shapes(pool4):
     g2, st2 = ver.verify_write2(wb2, 4, True)
     assert g2.cert_accept.all()
     ver.close()
+
+
+@pytest.mark.parametrize("with_flags", [False, True])
+def test_batcher_concurrent_callers(pool4, with_flags):
+    """mochi_batcher: 16 threads each block on their own messages; every caller
+    gets exactly the verdict the one-shot batch call gives, and the requests
+    were coalesced into far fewer GPU batches than messages."""
+    import threading
+
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 1200, first_cert=5000)
+    wb = W.encode_wire_batch(s)
+    if with_flags:
+        wb.op_flags = wb.op_flags.copy()
+        wb.op_flags[::7] = mh.OP_HAS_SVOC  # some ops not local -> WRONG_SHARD, never checked
+    ref, ref_st = ver.verify_write2(wb, 4, True)
+    b = mh.Batcher(ver, 4, True, max_msgs=128, max_wait_us=2000, with_op_flags=with_flags)
+    M = wb.n_msgs
+    res = [None] * M
+    msgs = [wb.wire[int(wb.msg_off[i]):int(wb.msg_off[i]) + int(wb.msg_len[i])].tobytes() for i in range(M)]
+    hashes = [wb.expected_hash[i].tobytes() for i in range(M)]
+    flags = [wb.op_flags[int(wb.op_flags_off[i]):int(wb.op_flags_off[i + 1])].tobytes() for i in range(M)]
+
+    def worker(t):
+        for i in range(t, M, 16):
+            res[i] = b.verify(msgs[i], hashes[i], flags[i] if with_flags else None)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    nb, nm = b.stats()
+    b.close()
+    assert nm == M and nb < M // 4
+    acc = np.array([r[0] for r in res])
+    np.testing.assert_array_equal(acc, ref.cert_accept)
+    np.testing.assert_array_equal(np.array([r[1] for r in res], np.uint8), ref.cert_reason)
+    np.testing.assert_array_equal(np.array([r[3] for r in res], np.uint8), ref_st)
+    ver.close()
