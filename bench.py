@@ -54,6 +54,8 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the Write2ToServer wire-path measurement")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the timed device-resident steps (no host-path / wire-path legs): the profiled run")
     ap.add_argument("--cache-dir", default=os.environ.get("MOCHI_CACHE", "/tmp/mochi_bench_cache"))
     return ap.parse_args()
 
@@ -166,8 +168,9 @@ def main():
             cpu["agrees_with_gpu"] = bool(np.array_equal(z["grant_flags"], host.grant_flags[:n]) and
                                           np.array_equal(z["cert_reason"], host.cert_reason[:z["cert_reason"].shape[0]]))
         # PCIe-inclusive host path (never the headline value)
-        host = host_path(ver, batch, R, strict)
-        wire = None if args.no_wire else wire_path(ver, pool, synth, R, strict, local_rank, stream, args)
+        host = None if args.headline_only else host_path(ver, batch, R, strict)
+        wire = None if (args.no_wire or args.headline_only) else wire_path(ver, pool, synth, R, strict, local_rank,
+                                                                          stream, args)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -206,7 +209,7 @@ def main():
             "stage_ms": {"prep_sha256": round(stage_ms[0], 4), "bucket": round(stage_ms[1], 4),
                          "rsa_pow": round(stage_ms[2], 4), "rsa_final": round(stage_ms[3], 4),
                          "tally": round(stage_ms[4], 4)},
-            "host_path_pcie_inclusive_grants_per_s": host["pinned_grants_per_s"],
+            "host_path_pcie_inclusive_grants_per_s": host["pinned_grants_per_s"] if host else None,
             "host_path": host,
             "write2_wire_path": wire,
             "correct_vs_ground_truth": all_ok,

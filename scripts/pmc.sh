@@ -4,7 +4,7 @@
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/pmc"; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=(python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --pool 1024)
+BENCH=(python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --headline-only --pool 1024)
 pass() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "k_rsa|k_grant_prep|k_tally" --output-format csv \
