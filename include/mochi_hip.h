@@ -365,6 +365,22 @@ int mochi_write2_decode(mochi_ctx* ctx, const mochi_write2_batch* batch, mochi_w
 void mochi_write2_decoded_free(mochi_write2_decoded* d);
 
 /* ------------------------------------------------------------------------
+ * Producer side on the device: SHA256withRSA over each grant's bytes with ONE
+ * server's private key (RSA-2048, CRT), the Write1 signing site
+ * (InMemoryDataStore.java:283-295, MochiProtocol.proto:123 TODO).  Output is
+ * bit-identical to mochi_sign_grants / OpenSSL (PKCS#1 v1.5 is deterministic).
+ * ------------------------------------------------------------------------ */
+typedef struct mochi_signer mochi_signer;
+mochi_signer* mochi_signer_create(int device, const char* pem_private_key);
+void mochi_signer_destroy(mochi_signer* s);
+/* Host memory, synchronous; sig_out: n * 256 bytes. */
+int mochi_sign_batch(mochi_signer* s, const uint8_t* grant_bytes, uint64_t grant_bytes_len, const uint64_t* grant_off,
+                     const uint32_t* grant_len, uint32_t n, uint8_t* sig_out);
+/* Device memory, asynchronous on `stream`. */
+int mochi_sign_batch_device(mochi_signer* s, const uint8_t* grant_bytes, const uint64_t* grant_off,
+                            const uint32_t* grant_len, uint32_t n, uint8_t* sig_out, void* stream);
+
+/* ------------------------------------------------------------------------
  * Micro-batcher: the blocking per-request call the Java handler keeps
  * (Write2ToServerRequestHandler.handle -> processWrite2ToServer on a 2..20
  * thread pool, MochiServer.java:36-40), coalesced across threads into one

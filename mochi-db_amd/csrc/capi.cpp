@@ -6,6 +6,9 @@
 // with one batched call over many certificates.
 #include <hip/hip_runtime.h>
 #include <openssl/bn.h>
+#include <openssl/core_names.h>
+#include <openssl/evp.h>
+#include <openssl/pem.h>
 
 #include <cstdarg>
 #include <cstdio>
@@ -1123,6 +1126,183 @@ int mochi_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const u
     decision[r] = d;
   }
   return MOCHI_OK;
+}
+
+}  // extern "C"
+
+// ---- device signer (rsa_sign.hip) --------------------------------------------
+struct mochi_signer {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void* d_key = nullptr;
+  std::mutex mu;
+  DevBuf dev_in, dev_sig;
+  PinnedBuf pin_in, pin_out;
+};
+
+namespace {
+
+int bn_limbs(const BIGNUM* v, uint32_t* x, int n_limbs) {
+  std::vector<uint8_t> le((size_t)n_limbs * 28 / 8 + 8, 0);
+  if (BN_num_bytes(v) > (int)le.size() - 8 || BN_bn2lebinpad(v, le.data(), (int)le.size()) < 0) return 0;
+  for (int j = 0; j < n_limbs; j++) {
+    const int bit = j * 28, by = bit >> 3, sh = bit & 7;
+    uint64_t w = 0;
+    for (int b = 0; b < 5; b++) w |= (uint64_t)le[by + b] << (8 * b);
+    x[j] = (uint32_t)(w >> sh) & 0x0FFFFFFFu;
+  }
+  return 1;
+}
+
+// -m^{-1} mod 2^28 from m's lowest 28-bit limb (odd): Newton on 32 bits
+uint32_t neg_inv28(uint32_t lo) {
+  uint32_t inv = 1;
+  for (int i = 0; i < 6; i++) inv *= 2u - lo * inv;
+  return (0u - inv) & 0x0FFFFFFFu;
+}
+
+}  // namespace
+
+extern "C" {
+
+mochi_signer* mochi_signer_create(int device, const char* pem) {
+  if (!pem) {
+    fail(MOCHI_EINVAL, "null key");
+    return nullptr;
+  }
+  BIO* bio = BIO_new_mem_buf(pem, -1);
+  EVP_PKEY* pk = bio ? PEM_read_bio_PrivateKey(bio, nullptr, nullptr, nullptr) : nullptr;
+  if (bio) BIO_free(bio);
+  BIGNUM *p = nullptr, *q = nullptr, *dp = nullptr, *dq = nullptr, *qi = nullptr;
+  bool ok = pk && EVP_PKEY_get_bits(pk) == 2048 && EVP_PKEY_get_bn_param(pk, OSSL_PKEY_PARAM_RSA_FACTOR1, &p) &&
+            EVP_PKEY_get_bn_param(pk, OSSL_PKEY_PARAM_RSA_FACTOR2, &q) &&
+            EVP_PKEY_get_bn_param(pk, OSSL_PKEY_PARAM_RSA_EXPONENT1, &dp) &&
+            EVP_PKEY_get_bn_param(pk, OSSL_PKEY_PARAM_RSA_EXPONENT2, &dq) &&
+            EVP_PKEY_get_bn_param(pk, OSSL_PKEY_PARAM_RSA_COEFFICIENT1, &qi);
+  if (pk) EVP_PKEY_free(pk);
+  ok = ok && BN_num_bits(p) <= 1024 && BN_num_bits(q) <= 1024 && BN_num_bits(dp) <= 1024 && BN_num_bits(dq) <= 1024 &&
+       BN_num_bits(dp) >= 2 && BN_num_bits(dq) >= 2;
+  constexpr int kLh = 37;
+  uint32_t lp[kLh], lq[kLh], r3p[kLh], r3q[kLh], qir[kLh], wdp[32], wdq[32], cpad[74];
+  BN_CTX* bc = BN_CTX_new();
+  BIGNUM *R = BN_new(), *t = BN_new(), *three = BN_new(), *cp = nullptr;
+  uint8_t cb[256];
+  memset(cb, 0xFF, sizeof cb);
+  static const uint8_t kDigestInfo[19] = {0x30, 0x31, 0x30, 0x0d, 0x06, 0x09, 0x60, 0x86, 0x48, 0x01,
+                                          0x65, 0x03, 0x04, 0x02, 0x01, 0x05, 0x00, 0x04, 0x20};
+  cb[0] = 0x00;
+  cb[1] = 0x01;
+  cb[256 - 32 - 19 - 1] = 0x00;
+  memcpy(cb + 256 - 32 - 19, kDigestInfo, 19);
+  memset(cb + 256 - 32, 0, 32);
+  cp = BN_bin2bn(cb, 256, nullptr);
+  ok = ok && bc && R && t && three && cp && BN_set_bit(R, 28 * kLh) && BN_set_word(three, 3);
+  ok = ok && bn_limbs(p, lp, kLh) && bn_limbs(q, lq, kLh);
+  ok = ok && BN_mod_exp(t, R, three, p, bc) && bn_limbs(t, r3p, kLh);
+  ok = ok && BN_mod_exp(t, R, three, q, bc) && bn_limbs(t, r3q, kLh);
+  ok = ok && BN_mod_mul(t, qi, R, p, bc) && bn_limbs(t, qir, kLh);
+  ok = ok && bn_limbs(cp, cpad, 74);
+  uint8_t le[128];
+  ok = ok && BN_bn2lebinpad(dp, le, 128) == 128;
+  if (ok)
+    for (int i = 0; i < 32; i++) wdp[i] = (uint32_t)le[4 * i] | (uint32_t)le[4 * i + 1] << 8 | (uint32_t)le[4 * i + 2] << 16 | (uint32_t)le[4 * i + 3] << 24;
+  ok = ok && BN_bn2lebinpad(dq, le, 128) == 128;
+  if (ok)
+    for (int i = 0; i < 32; i++) wdq[i] = (uint32_t)le[4 * i] | (uint32_t)le[4 * i + 1] << 8 | (uint32_t)le[4 * i + 2] << 16 | (uint32_t)le[4 * i + 3] << 24;
+  std::vector<uint8_t> host(mochi::sign_key_bytes());
+  if (ok)
+    mochi::sign_key_set(host.data(), lp, lq, r3p, r3q, qir, wdp, wdq, cpad, neg_inv28(lp[0]), neg_inv28(lq[0]),
+                        (uint32_t)BN_num_bits(dp), (uint32_t)BN_num_bits(dq));
+  for (BIGNUM* b : {p, q, dp, dq, qi, R, t, three, cp}) BN_clear_free(b);
+  BN_CTX_free(bc);
+  if (!ok) {
+    fail(MOCHI_EINVAL, "not an RSA-2048 private key with CRT parameters");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    fail(MOCHI_ENODEV, "device %d not available", device);
+    return nullptr;
+  }
+  mochi_signer* s = new mochi_signer;
+  s->device = device;
+  int save = 0;
+  (void)hipGetDevice(&save);
+  ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
+       hipMalloc(&s->d_key, host.size()) == hipSuccess &&
+       hipMemcpy(s->d_key, host.data(), host.size(), hipMemcpyHostToDevice) == hipSuccess;
+  memset(host.data(), 0, host.size());
+  (void)hipSetDevice(save);
+  if (!ok) {
+    fail(MOCHI_EHIP, "signer setup failed");
+    mochi_signer_destroy(s);
+    return nullptr;
+  }
+  return s;
+}
+
+void mochi_signer_destroy(mochi_signer* s) {
+  if (!s) return;
+  int save = 0;
+  (void)hipGetDevice(&save);
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->d_key) {
+    (void)hipMemset(s->d_key, 0, mochi::sign_key_bytes());  // private key material
+    (void)hipFree(s->d_key);
+  }
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+  (void)hipSetDevice(save);
+}
+
+int mochi_sign_batch_device(mochi_signer* s, const uint8_t* grant_bytes, const uint64_t* grant_off,
+                            const uint32_t* grant_len, uint32_t n, uint8_t* sig_out, void* stream) {
+  if (!s || (n && (!grant_bytes || !grant_off || !grant_len || !sig_out))) return fail(MOCHI_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(s->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice");
+  const hipError_t e = mochi::launch_rsa_sign(grant_bytes, grant_off, grant_len, n, s->d_key, sig_out,
+                                              (hipStream_t)stream);
+  (void)hipSetDevice(save);
+  return e == hipSuccess ? MOCHI_OK : fail(MOCHI_EHIP, "k_rsa_sign: %s", hipGetErrorString(e));
+}
+
+int mochi_sign_batch(mochi_signer* s, const uint8_t* grant_bytes, uint64_t grant_bytes_len, const uint64_t* grant_off,
+                     const uint32_t* grant_len, uint32_t n, uint8_t* sig_out) {
+  if (!s || (n && (!grant_bytes || !grant_off || !grant_len || !sig_out))) return fail(MOCHI_EINVAL, "null argument");
+  for (uint32_t i = 0; i < n; i++)
+    if (grant_off[i] > grant_bytes_len || grant_len[i] > grant_bytes_len - grant_off[i])
+      return fail(MOCHI_EINVAL, "grant %u lies outside grant_bytes", i);
+  if (n == 0) return MOCHI_OK;
+  std::lock_guard<std::mutex> lk(s->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  if (hipSetDevice(s->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice");
+  const size_t o_off = align_up(grant_bytes_len, 256), o_len = o_off + align_up(8 * (size_t)n, 256),
+               total = o_len + align_up(4 * (size_t)n, 256), sig_bytes = (size_t)MOCHI_RSA_BYTES * n;
+  int rc;
+  if ((rc = s->pin_in.ensure(total)) || (rc = s->dev_in.ensure(total)) || (rc = s->pin_out.ensure(sig_bytes)) ||
+      (rc = s->dev_sig.ensure(sig_bytes))) {
+    (void)hipSetDevice(save);
+    return rc;
+  }
+  uint8_t* pin = (uint8_t*)s->pin_in.p;
+  par_memcpy(pin, grant_bytes, grant_bytes_len);
+  memcpy(pin + o_off, grant_off, 8 * (size_t)n);
+  memcpy(pin + o_len, grant_len, 4 * (size_t)n);
+  uint8_t* din = s->dev_in.as<uint8_t>();
+  hipStream_t st = s->stream;
+  hipError_t e = hipMemcpyAsync(din, pin, total, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = mochi::launch_rsa_sign(din, (const uint64_t*)(din + o_off), (const uint32_t*)(din + o_len), n, s->d_key,
+                               s->dev_sig.as<uint8_t>(), st);
+  if (e == hipSuccess) e = hipMemcpyAsync(s->pin_out.p, s->dev_sig.p, sig_bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) memcpy(sig_out, s->pin_out.p, sig_bytes);
+  (void)hipSetDevice(save);
+  return e == hipSuccess ? MOCHI_OK : fail(MOCHI_EHIP, "sign batch: %s", hipGetErrorString(e));
 }
 
 }  // extern "C"

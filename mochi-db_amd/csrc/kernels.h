@@ -92,6 +92,14 @@ hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reas
                            hipStream_t stream);
 
 hipError_t launch_verify(const LaunchArgs& a, hipStream_t stream);
+
+// Device signer (rsa_sign.hip).
+size_t sign_key_bytes();
+void sign_key_set(void* dst, const uint32_t* p, const uint32_t* q, const uint32_t* r3p, const uint32_t* r3q,
+                  const uint32_t* qinv_r, const uint32_t* dp, const uint32_t* dq, const uint32_t* cpad, uint32_t p0inv,
+                  uint32_t q0inv, uint32_t dp_bits, uint32_t dq_bits);
+hipError_t launch_rsa_sign(const uint8_t* blob, const uint64_t* goff, const uint32_t* glen, uint32_t n,
+                           const void* key, uint8_t* sig, hipStream_t stream);
 hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t stream);
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream);
 void launch_rsa_final(const LaunchArgs& a, hipStream_t stream);

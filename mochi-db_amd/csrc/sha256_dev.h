@@ -1,0 +1,84 @@
+// sha256_dev.h — SHA-256 (FIPS 180-4) of one lane's byte string, shared by the
+// grant-prep kernel (kernels.hip) and the device signer (rsa_sign.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mochi {
+
+// ---------------------------------------------------------------------------
+// SHA-256 (FIPS 180-4) over one lane's grant bytes.
+// ---------------------------------------------------------------------------
+static __constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t sha_rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+// Big-endian message word at byte position p (multiple of 4) of the padded message.
+__device__ __forceinline__ uint32_t sha_word(const uint8_t* base, uint32_t p, uint32_t len, uint32_t total) {
+  if (p + 4 <= len) {
+    const uintptr_t addr = (uintptr_t)(base + p);
+    const uint32_t* wp = (const uint32_t*)(addr & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(addr & 3);
+    const uint32_t w0 = wp[0];
+    const uint32_t w1 = sh ? wp[1] : 0u;  // holds message byte p+3 when sh != 0
+    const uint32_t le = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh));
+    return __builtin_bswap32(le);
+  }
+  if (p + 8 == total) return 0;  // high half of the 64-bit bit length (len < 2^29)
+  if (p + 4 == total) return len << 3;
+  uint32_t v = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t i = p + q;
+    uint32_t byte = 0;
+    if (i < len) byte = base[i];
+    else if (i == len) byte = 0x80;
+    v = (v << 8) | byte;
+  }
+  return v;
+}
+
+__device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8]) {
+  h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
+  h[4] = 0x510e527f; h[5] = 0x9b05688c; h[6] = 0x1f83d9ab; h[7] = 0x5be0cd19;
+  const uint32_t nblocks = (len + 9 + 63) >> 6;
+  const uint32_t total = nblocks << 6;
+#pragma unroll 1
+  for (uint32_t blk = 0; blk < nblocks; blk++) {
+    uint32_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) w[t] = sha_word(base, blk * 64 + 4 * t, len, total);
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+        const uint32_t s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
+        const uint32_t s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
+        wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+        w[t & 15] = wt;
+      }
+      const uint32_t S1 = sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25);
+      const uint32_t ch = (e & f) ^ (~e & g);
+      const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
+      const uint32_t S0 = sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22);
+      const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+      const uint32_t t2 = S0 + mj;
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+}
+
+}  // namespace mochi

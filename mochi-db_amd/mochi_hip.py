@@ -146,6 +146,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_verify_write2_device.argtypes = [vp, vp, vp, vp, vp, vp]
     lib.mochi_write2_decode.argtypes = [vp, vp, vp]
     lib.mochi_write2_decoded_free.argtypes = [vp]
+    lib.mochi_signer_create.restype = vp
+    lib.mochi_signer_create.argtypes = [ctypes.c_int, ctypes.c_char_p]
+    lib.mochi_signer_destroy.argtypes = [vp]
+    lib.mochi_sign_batch.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, u32, vp]
+    lib.mochi_sign_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     lib.mochi_batcher_create.restype = vp
     lib.mochi_batcher_create.argtypes = [vp, vp, u32, u32, ctypes.c_int]
     lib.mochi_batcher_verify.argtypes = [vp, vp, u32, vp, u32, vp, vp]
@@ -755,5 +760,38 @@ class Batcher:
     def close(self):
         if self.h:
             self.lib.mochi_batcher_destroy(self.h)
+            self.h = None
+
+
+class DeviceSigner:
+    """Producer-side SHA256withRSA on the device with one server's private key
+    (mochi_signer_*; bit-identical to sign_grants / OpenSSL)."""
+
+    def __init__(self, pem_private_key: bytes, device: int = 0):
+        self.lib = load_library()
+        self.h = self.lib.mochi_signer_create(int(device), pem_private_key)
+        if not self.h:
+            raise MochiError(f"mochi_signer_create: {_err(self.lib)}")
+
+    def sign(self, grant_bytes: np.ndarray, grant_off: np.ndarray, grant_len: np.ndarray) -> np.ndarray:
+        blob = np.ascontiguousarray(grant_bytes, np.uint8)
+        off = np.ascontiguousarray(grant_off, np.uint64)
+        ln = np.ascontiguousarray(grant_len, np.uint32)
+        n = int(off.shape[0])
+        out = np.zeros((n, RSA_BYTES), np.uint8)
+        rc = self.lib.mochi_sign_batch(self.h, _ptr(blob), blob.nbytes, _ptr(off), _ptr(ln), n, _ptr(out))
+        if rc != OK:
+            raise MochiError(f"mochi_sign_batch rc={rc}: {_err(self.lib)}")
+        return out
+
+    def sign_device(self, blob_t, off_t, len_t, n: int, sig_t, stream: int = 0) -> None:
+        rc = self.lib.mochi_sign_batch_device(self.h, blob_t.data_ptr(), off_t.data_ptr(), len_t.data_ptr(), n,
+                                              sig_t.data_ptr(), stream)
+        if rc != OK:
+            raise MochiError(f"mochi_sign_batch_device rc={rc}: {_err(self.lib)}")
+
+    def close(self):
+        if self.h:
+            self.lib.mochi_signer_destroy(self.h)
             self.h = None
 
