@@ -168,9 +168,10 @@ def main():
             cpu["agrees_with_gpu"] = bool(np.array_equal(z["grant_flags"], host.grant_flags[:n]) and
                                           np.array_equal(z["cert_reason"], host.cert_reason[:z["cert_reason"].shape[0]]))
         # PCIe-inclusive host path (never the headline value)
-        host = None if args.headline_only else host_path(ver, batch, R, strict)
-        wire = None if (args.no_wire or args.headline_only) else wire_path(ver, pool, synth, R, strict, local_rank,
-                                                                          stream, args)
+        extras = world == 1 and not args.headline_only  # side measurements: single-GPU runs only
+        host = host_path(ver, batch, R, strict) if extras else None
+        wire = wire_path(ver, pool, synth, R, strict, local_rank, stream, args) if extras and not args.no_wire else None
+        signing = sign_path(pool, batch, local_rank, stream, args) if extras else None
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -212,6 +213,7 @@ def main():
             "host_path_pcie_inclusive_grants_per_s": host["pinned_grants_per_s"] if host else None,
             "host_path": host,
             "write2_wire_path": wire,
+            "producer_signing": signing,
             "correct_vs_ground_truth": all_ok,
             "cpu_baseline": cpu,
             "wall_s": round(wall_max, 4),
@@ -284,6 +286,44 @@ def wire_path(ver, pool, synth, R, strict, dev, stream, args):
             "wire_bytes": int(wb.wire.nbytes), "verdicts_equal_soa_path": same,
             "host_encode_s": round(enc_s, 2),
             "note": "Write2ToServer bodies resident in HBM; includes one host wait on the decoded totals per step"}
+
+
+def sign_path(pool, batch, dev, stream, args, n_gpu=262144, n_cpu=16384):
+    """Producer side (Write1 signing site): SHA256withRSA-2048 of grants with one
+    server key on the device (k_rsa_sign, CRT) vs OpenSSL on the host cores."""
+    import numpy as np
+    import torch
+
+    import mochi_hip as mh
+
+    n = min(n_gpu, batch.n_grants)
+    off = np.ascontiguousarray(batch.grant_off[:n], np.uint64)
+    ln = np.ascontiguousarray(batch.grant_len[:n], np.uint32)
+    d = torch.device("cuda", dev)
+    blob_t = torch.from_numpy(np.ascontiguousarray(batch.grant_bytes)).to(d)
+    off_t = torch.from_numpy(off.view(np.int64)).to(d)
+    len_t = torch.from_numpy(ln.view(np.int32)).to(d)
+    sig_t = torch.empty((n, 256), dtype=torch.uint8, device=d)
+    s = mh.DeviceSigner(pool.key_pems[0], dev)
+    s.sign_device(blob_t, off_t, len_t, n, sig_t, stream.cuda_stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 3
+    e0.record(stream)
+    for _ in range(reps):
+        s.sign_device(blob_t, off_t, len_t, n, sig_t, stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t_gpu = e0.elapsed_time(e1) / 1e3 / reps
+    got = sig_t[:64].cpu().numpy()
+    s.close()
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    ref = mh.sign_grants(pool.key_pems[0], batch.grant_bytes, off[:n_cpu], ln[:n_cpu], threads)
+    t_cpu = time.perf_counter() - t0
+    return {"gpu_signatures_per_s": round(n / t_gpu, 1), "gpu_ms_per_launch": round(t_gpu * 1e3, 3), "grants": n,
+            "cpu_signatures_per_s": round(n_cpu / t_cpu, 1), "cpu_threads": threads, "cpu_sample": n_cpu,
+            "bit_exact_sample": bool(np.array_equal(got, ref[:64]))}
 
 
 def run_cpu_baseline(args, R, k, flags_out):
