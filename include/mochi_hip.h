@@ -187,11 +187,13 @@ int mochi_rsa_public_op(mochi_ctx* ctx, uint32_t n, const uint8_t* sig_be, const
                         uint32_t* out_z);
 
 /*
- * Per-stage device timing.  While profiling is on, every verify call records
- * hipEvents between its stages on the stream it runs on; mochi_ctx_read_profile
- * waits for them and returns the SUM over calls since the last read, per stage:
- * [0] grant prep (parse + SHA-256), [1] signer bucketing, [2] k_rsa_pow,
- * [3] k_rsa_final (+ bitmap pack), [4] k_tally.  n_stages <= 5.
+ * Per-stage device timing.  While profiling is on, every verify call records a
+ * (start, end) hipEvent pair around each stage on the stream the stage runs
+ * on; mochi_ctx_read_profile waits for them and returns the SUM over calls
+ * since the last read, per stage: [0] grant prep (parse + SHA-256; it runs on
+ * the context's aux stream, concurrently with [1] and [2]), [1] signer
+ * bucketing, [2] k_rsa_pow, [3] k_rsa_final (+ bitmap pack), [4] k_tally.
+ * n_stages <= 5.
  */
 int mochi_ctx_set_profiling(mochi_ctx* ctx, int on);
 int mochi_ctx_read_profile(mochi_ctx* ctx, float* stage_ms, uint32_t n_stages, uint32_t* n_calls);

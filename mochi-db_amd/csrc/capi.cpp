@@ -169,6 +169,8 @@ struct mochi_ctx {
   DevBuf dev_in, dev_out;
   PinnedBuf pin_in, pin_out;
   hipStream_t s_in = nullptr, s_out = nullptr;  // host-path copy streams
+  hipStream_t aux = nullptr;                     // grant prep, overlapped with bucketing + k_rsa_pow
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<hipEvent_t> chunk_ev;              // host-path chunk hand-offs
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float last_ms[3] = {0, 0, 0};  // first upload, compute span, last download of the last host-path call
@@ -236,6 +238,9 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
   (void)hipGetDevice(&save);
   bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) == hipSuccess &&
             hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_keys, sizeof(mochi::KeyEntry) * n_keys) == hipSuccess &&
             hipMemcpy(c->d_keys, table.data(), sizeof(mochi::KeyEntry) * n_keys, hipMemcpyHostToDevice) == hipSuccess;
@@ -259,7 +264,11 @@ void mochi_ctx_destroy(mochi_ctx* c) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->chunk_ev) (void)hipEventDestroy(e);
+  if (c->aux) (void)hipStreamSynchronize(c->aux);
   if (c->s_in) (void)hipStreamDestroy(c->s_in);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->s_out) (void)hipStreamDestroy(c->s_out);
   if (c->d_keys) (void)hipFree(c->d_keys);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -352,8 +361,11 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.cert_accept_bits = o->cert_accept_bits;
   a.cert_reason = o->cert_reason;
   a.cert_fail_op = o->cert_fail_op;
+  a.aux = c->aux;
+  a.ev_fork = c->ev_fork;
+  a.ev_join = c->ev_join;
   if (c->profiling) {
-    std::vector<hipEvent_t> evs(mochi::kProfStages + 1, nullptr);
+    std::vector<hipEvent_t> evs(2 * mochi::kProfStages, nullptr);
     for (auto& e : evs) HIP_TRY(hipEventCreate(&e));
     c->prof_sets.push_back(evs);
     a.prof_events = c->prof_sets.back().data();
@@ -1013,10 +1025,11 @@ int mochi_ctx_read_profile(mochi_ctx* c, float* stage_ms, uint32_t n_stages, uin
   for (uint32_t i = 0; i < n_stages; i++) stage_ms[i] = 0.f;
   uint32_t calls = 0;
   for (auto& evs : c->prof_sets) {
-    if (hipEventSynchronize(evs.back()) != hipSuccess) return fail(MOCHI_EHIP, "hipEventSynchronize failed");
+    for (auto e : evs)
+      if (hipEventSynchronize(e) != hipSuccess) return fail(MOCHI_EHIP, "hipEventSynchronize failed");
     for (uint32_t i = 0; i < n_stages && i < (uint32_t)mochi::kProfStages; i++) {
       float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, evs[i], evs[i + 1]);
+      (void)hipEventElapsedTime(&ms, evs[2 * i], evs[2 * i + 1]);  // (start, end) of stage i
       stage_ms[i] += ms;
     }
     for (auto e : evs) (void)hipEventDestroy(e);

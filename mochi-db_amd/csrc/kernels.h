@@ -43,7 +43,12 @@ struct LaunchArgs {
   // mochi_rsa_public_op only: raw s^65537 mod n words [N][64] (else null)
   uint32_t* dbg_y;
   bool skip_prep_tally;
-  // optional per-stage timing: kProfStages + 1 events recorded on the launch stream
+  // grant prep runs on `aux` (forked from / joined back to the launch stream
+  // with ev_fork / ev_join) so it overlaps bucketing and k_rsa_pow; null = inline
+  hipStream_t aux;
+  hipEvent_t ev_fork, ev_join;
+  // optional per-stage timing: a (start, end) event pair per stage, recorded on
+  // the stream the stage runs on
   hipEvent_t* prof_events;
 };
 

@@ -235,14 +235,30 @@ hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint
 
 hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   const uint32_t N = a.n_grants, C = a.n_certs;
-  auto mark = [&](int i) {
-    if (a.prof_events) (void)hipEventRecord(a.prof_events[i], st);
+  auto mark = [&](int stage, bool end, hipStream_t s) {
+    if (a.prof_events) (void)hipEventRecord(a.prof_events[2 * stage + (end ? 1 : 0)], s);
   };
-  mark(0);
-  if (N && !a.skip_prep_tally)
-    hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, st, a.blob, a.grant_off, a.grant_len, N,
+  // grant prep (parse + SHA-256) only feeds k_rsa_final and k_tally, so it runs
+  // beside bucketing + k_rsa_pow on the aux stream and fills their idle issue
+  // slots (it is latency-bound); the launch stream joins it before k_rsa_final
+  const bool prep = N && !a.skip_prep_tally;
+  const bool fork = prep && a.aux;
+  hipStream_t ps = fork ? a.aux : st;
+  if (fork) {
+    hipError_t e = hipEventRecord(a.ev_fork, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(a.aux, a.ev_fork, 0);
+    if (e != hipSuccess) return e;
+  }
+  mark(kStagePrep, false, ps);
+  if (prep)
+    hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, a.blob, a.grant_off, a.grant_len, N,
                        a.digest, a.ts, nullptr, a.hash_off, a.hash_len, a.flags);
-  mark(1 + kStagePrep);
+  mark(kStagePrep, true, ps);
+  if (fork) {
+    hipError_t e = hipEventRecord(a.ev_join, a.aux);
+    if (e != hipSuccess) return e;
+  }
+  mark(kStageBucket, false, st);
   if (N) {
     hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, st);
     if (e != hipSuccess) return e;
@@ -255,21 +271,28 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_bucket_scatter, dim3(cdiv(N, 256)), dim3(256), 2 * lds, st, a.signer, N, a.n_keys, a.cursor,
                        a.perm);
   }
-  mark(1 + kStageBucket);
+  mark(kStageBucket, true, st);
+  mark(kStagePow, false, st);
   if (N) launch_rsa_pow(a, st);
-  mark(1 + kStagePow);
+  mark(kStagePow, true, st);
+  if (fork) {
+    hipError_t e = hipStreamWaitEvent(st, a.ev_join, 0);
+    if (e != hipSuccess) return e;
+  }
+  mark(kStageFinal, false, st);
   if (N) {
     launch_rsa_final(a, st);
     if (a.grant_valid_bits)
       hipLaunchKernelGGL(k_pack_bits, dim3(cdiv(N, 256)), dim3(256), 0, st, a.flags, N, (uint8_t)MOCHI_GRANT_SIG_OK,
                          a.grant_valid_bits);
   }
-  mark(1 + kStageFinal);
+  mark(kStageFinal, true, st);
+  mark(kStageTally, false, st);
   if (C && !a.skip_prep_tally)
     hipLaunchKernelGGL(k_tally, dim3(cdiv(C, 256)), dim3(256), 0, st, a.cert_grant_off, a.cert_op_off, a.grant_key,
                        a.op_key, a.op_flags, a.flags, a.ts, a.blob, a.hash_off, a.hash_len, a.expected_hash, C,
                        a.majority, a.strict_gt, a.cert_accept_bits, a.cert_reason, a.cert_fail_op);
-  mark(1 + kStageTally);
+  mark(kStageTally, true, st);
   return hipGetLastError();
 }
 
