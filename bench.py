@@ -50,7 +50,10 @@ def parse_args():
     ap.add_argument("--replication", type=int, default=4)
     ap.add_argument("--ops-per-txn", type=int, default=1)
     ap.add_argument("--client-predicate", action="store_true", help="count >= M instead of the server's count > M")
-    ap.add_argument("--pool", type=int, default=4096, help="unique signed grant templates per server")
+    ap.add_argument("--pool", type=int, default=4096, help="template pool size (--workload pool)")
+    ap.add_argument("--workload", choices=("unique", "pool"), default="unique",
+                    help="unique: SURVEY §8d stream, every certificate's grant bytes distinct, signed on the GPU; "
+                         "pool: grants sampled from a CPU-signed template pool (cache-resident grant bytes)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the Write2ToServer wire-path measurement")
@@ -75,11 +78,14 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     R, k = args.replication, args.ops_per_txn
     strict = not args.client_predicate
-    # CPU baseline first (rank 0, N = 1 only), in a child process that never touches the GPU
-    cpu = None
+    # CPU baseline (rank 0, N = 1 only): a child process started BEFORE this
+    # process touches the GPU (it forks its workers and must hold no HIP
+    # state); it waits for the batch file written below and times the oracle.
+    cpu_child = None
     cpu_flags = os.path.join(args.cache_dir, "cpu_baseline_flags.npz")
+    batch_file = os.path.join(args.cache_dir, f"bench_batch_{os.getpid()}.npz")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = run_cpu_baseline(args, R, k, cpu_flags)
+        cpu_child = start_cpu_baseline(args, R, k, cpu_flags, batch_file if args.workload == "unique" else None)
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
@@ -87,20 +93,38 @@ def main():
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    # pool: rank 0 signs it once, the others load the cache file
-    if rank == 0:
-        pool = W.build_pool(R=R, k=k, P=args.pool, P_f=256, cache_dir=args.cache_dir)
-    if dist is not None:
-        dist.barrier()
-    if rank != 0:
-        pool = W.build_pool(R=R, k=k, P=args.pool, P_f=256, cache_dir=args.cache_dir)
-
     C = W.n_certs_for_grants(args.grants_per_gpu, R, k)
-    synth = W.make_batch(pool, C, first_cert=rank * C)
+    if args.workload == "unique":
+        # SURVEY §8d stream, unique grant bytes per certificate, signed on this GPU (k_rsa_sign)
+        t_gen = time.perf_counter()
+        synth = W.make_batch_unique(R, C, k, first_cert=rank * C, device=local_rank)
+        gen_s = time.perf_counter() - t_gen
+        moduli = [mh.pem_modulus(p) for p in W.load_keys(R)]
+        pool = None
+        if cpu_child is not None:
+            os.makedirs(args.cache_dir, exist_ok=True)
+            tmp = batch_file + ".tmp.npz"
+            W.save_batch(tmp, synth)
+            os.replace(tmp, batch_file)
+    else:
+        # template pool: rank 0 signs it once on the CPU, the others load the cache file
+        t_gen = time.perf_counter()
+        if rank == 0:
+            pool = W.build_pool(R=R, k=k, P=args.pool, P_f=256, cache_dir=args.cache_dir)
+        if dist is not None:
+            dist.barrier()
+        if rank != 0:
+            pool = W.build_pool(R=R, k=k, P=args.pool, P_f=256, cache_dir=args.cache_dir)
+        synth = W.make_batch(pool, C, first_cert=rank * C)
+        gen_s = time.perf_counter() - t_gen
+        moduli = pool.moduli
+    cpu = finish_cpu_baseline(cpu_child) if cpu_child is not None else None
+    if os.path.exists(batch_file):
+        os.remove(batch_file)
     batch = synth.batch
     N = batch.n_grants
 
-    ver = mh.Verifier(pool.moduli, device=local_rank)
+    ver = mh.Verifier(moduli, device=local_rank)
     dev = mh.DeviceBatch(batch, local_rank)
     out = mh.DeviceVerdicts(dev.n_grants, dev.n_certs, local_rank, full=True)
     stream = torch.cuda.current_stream()
@@ -171,7 +195,7 @@ def main():
         extras = world == 1 and not args.headline_only  # side measurements: single-GPU runs only
         host = host_path(ver, batch, R, strict) if extras else None
         wire = wire_path(ver, pool, synth, R, strict, local_rank, stream, args) if extras and not args.no_wire else None
-        signing = sign_path(pool, batch, local_rank, stream, args) if extras else None
+        signing = sign_path(W.load_keys(1)[0], batch, local_rank, stream, args) if extras else None
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -187,7 +211,11 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"C2: {N} synthetic SHA256withRSA-2048 signed grants per GPU, R={R} (f={R // 3}), "
-                            f"k={k} op/txn, {'server' if strict else 'client'} quorum predicate, 2.75% fault mix",
+                            f"k={k} op/txn, {'server' if strict else 'client'} quorum predicate, 2.75% fault mix, "
+                            + ("unique grant bytes per certificate (SURVEY §8d stream; signed on the GPU by "
+                               "k_rsa_sign, bit-identical to OpenSSL)" if args.workload == "unique" else
+                               f"grants sampled from a {args.pool}-template CPU-signed pool"),
+                "workload_generation_s": round(gen_s, 2),
                 "grants_per_gpu": N,
                 "certs_per_gpu": C,
                 "replication_factor": R,
@@ -288,7 +316,7 @@ def wire_path(ver, pool, synth, R, strict, dev, stream, args):
             "note": "Write2ToServer bodies resident in HBM; includes one host wait on the decoded totals per step"}
 
 
-def sign_path(pool, batch, dev, stream, args, n_gpu=262144, n_cpu=16384):
+def sign_path(pem, batch, dev, stream, args, n_gpu=262144, n_cpu=16384):
     """Producer side (Write1 signing site): SHA256withRSA-2048 of grants with one
     server key on the device (k_rsa_sign, CRT) vs OpenSSL on the host cores."""
     import numpy as np
@@ -304,7 +332,7 @@ def sign_path(pool, batch, dev, stream, args, n_gpu=262144, n_cpu=16384):
     off_t = torch.from_numpy(off.view(np.int64)).to(d)
     len_t = torch.from_numpy(ln.view(np.int32)).to(d)
     sig_t = torch.empty((n, 256), dtype=torch.uint8, device=d)
-    s = mh.DeviceSigner(pool.key_pems[0], dev)
+    s = mh.DeviceSigner(pem, dev)
     s.sign_device(blob_t, off_t, len_t, n, sig_t, stream.cuda_stream)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -319,29 +347,38 @@ def sign_path(pool, batch, dev, stream, args, n_gpu=262144, n_cpu=16384):
     s.close()
     threads = min(16, os.cpu_count() or 1)
     t0 = time.perf_counter()
-    ref = mh.sign_grants(pool.key_pems[0], batch.grant_bytes, off[:n_cpu], ln[:n_cpu], threads)
+    ref = mh.sign_grants(pem, batch.grant_bytes, off[:n_cpu], ln[:n_cpu], threads)
     t_cpu = time.perf_counter() - t0
     return {"gpu_signatures_per_s": round(n / t_gpu, 1), "gpu_ms_per_launch": round(t_gpu * 1e3, 3), "grants": n,
             "cpu_signatures_per_s": round(n_cpu / t_cpu, 1), "cpu_threads": threads, "cpu_sample": n_cpu,
             "bit_exact_sample": bool(np.array_equal(got, ref[:64]))}
 
 
-def run_cpu_baseline(args, R, k, flags_out):
-    """The oracle (OpenSSL SHA256withRSA verify + the restated quorum logic) timed
-    on this host's cores over a bounded sample of the same workload, in a child
-    process (tests/cpu_baseline.py) that forks its workers without any HIP state."""
+def start_cpu_baseline(args, R, k, flags_out, batch_file):
+    """The oracle (OpenSSL SHA256withRSA verify + the restated quorum logic)
+    timed on this host's cores over a bounded sample of the same workload, in a
+    child process (tests/cpu_baseline.py) that forks its workers without any
+    HIP state; with --workload unique it waits for the batch file the parent
+    writes after generating the stream on the GPU."""
     import subprocess
 
     os.makedirs(args.cache_dir, exist_ok=True)
     cmd = [sys.executable, os.path.join(ROOT, "tests", "cpu_baseline.py"), "--replication", str(R), "--ops-per-txn",
            str(k), "--pool", str(args.pool), "--cache-dir", args.cache_dir, "--seconds", str(args.cpu_seconds),
            "--max-certs", str(max(1, args.grants_per_gpu // (R * k))), "--flags-out", flags_out]
+    if batch_file:
+        cmd += ["--batch-file", batch_file]
     if args.client_predicate:
         cmd.append("--client-predicate")
+    return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+
+def finish_cpu_baseline(child):
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
-        return json.loads(r.stdout.strip().splitlines()[-1])
+        out, err = child.communicate(timeout=900)
+        return json.loads(out.strip().splitlines()[-1])
     except Exception as ex:  # the baseline is reported, never required
+        child.kill()
         return {"error": f"cpu baseline failed: {ex}"}
 
 

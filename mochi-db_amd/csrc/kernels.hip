@@ -121,17 +121,30 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint16_t* __restri
 // Certificate tally (lane = certificate).  Restates oracle_tally, i.e.
 // InMemoryDataStore.java:613-640 then :576-611 (verdict part).
 // ---------------------------------------------------------------------------
+// 32 words of a 128-byte string at any byte alignment: 33 (or 32) aligned
+// word loads issued back to back and funnel-shifted; never touches a word that
+// holds no byte of the string.
+__device__ __forceinline__ void load128(const uint8_t* p, uint32_t (&w)[32]) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* wp = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  uint32_t raw[33];
+#pragma unroll
+  for (int i = 0; i < 32; i++) raw[i] = wp[i];
+  raw[32] = sh ? wp[32] : 0u;
+#pragma unroll
+  for (int i = 0; i < 32; i++) w[i] = (uint32_t)((((uint64_t)raw[i + 1] << 32) | raw[i]) >> (8 * sh));
+}
+
 __device__ bool hash_matches(const uint8_t* __restrict__ blob, uint64_t off, uint32_t len,
                              const uint8_t* __restrict__ expected) {
   if (len != MOCHI_TXN_HASH_BYTES) return false;
-  const uint8_t* p = blob + off;
+  uint32_t a[32], e[32];
+  load128(blob + off, a);
+  load128(expected, e);
   uint32_t diff = 0;
-#pragma unroll 4
-  for (int q = 0; q < MOCHI_TXN_HASH_BYTES / 4; q++) {
-    const uint32_t a = sha_word(p, 4 * q, MOCHI_TXN_HASH_BYTES, 0xFFFFFFFFu);
-    const uint32_t e = sha_word(expected, 4 * q, MOCHI_TXN_HASH_BYTES, 0xFFFFFFFFu);
-    diff |= a ^ e;
-  }
+#pragma unroll
+  for (int q = 0; q < 32; q++) diff |= a[q] ^ e[q];
   return diff == 0;
 }
 

@@ -394,3 +394,126 @@ def server_id_table(n: int, server_ids=None):
     off = np.zeros(n + 1, np.uint32)
     np.cumsum([len(x.encode()) for x in ids], out=off[1:])
     return np.frombuffer(blob, np.uint8).copy(), off
+
+
+# ---------------------------------------------------------------------------
+# SURVEY.md §8d's per-certificate stream with UNIQUE grant bytes, signed on the
+# device (k_rsa_sign, bit-identical to OpenSSL): certificate c has objectId
+# DEMO_KEY_STRESS_TEST_{(c*k + j) mod 200} per op j, timestamp
+# 1000*(c mod 64) + (h(c) mod 1000) and transactionHash = hex SHA-512 of
+# "txn-{c}".  Every replica signs the same grant bytes (one copy in the blob,
+# certificate order); fault variants get their own copy.  This is the bench
+# workload: unlike the template pool, its grant bytes (~150 MB per 1M grants)
+# do not sit in cache.
+# ---------------------------------------------------------------------------
+def make_batch_unique(R: int, n_certs: int, k: int = 1, first_cert: int = 0, seed: int = SEED, faults: bool = True,
+                      device: int = 0, key_dir: str = DEFAULT_KEY_DIR,
+                      local_flags: int = OP_LOCAL | OP_HAS_SVOC) -> Synth:
+    import mochi_hip as mh
+
+    pems = load_keys(R, key_dir)
+    C = n_certs
+    cidx = np.arange(first_cert, first_cert + C, dtype=np.uint64)
+    fault = np.zeros(C, np.int64)
+    if faults:
+        u = (_h(seed, 2, cidx) % np.uint64(10000)).astype(np.int64)
+        lo = 0
+        for hi, f in _FAULT_TABLE:
+            fault[(u >= lo) & (u < hi)] = f
+            lo = hi
+    rf = (_h(seed, 3, cidx) % np.uint64(R)).astype(np.int64)
+    rf[fault == FAULT_G0_HASH] = 0
+    rf[fault == FAULT_G1_HASH] = 1 % R
+    hts = (_h(seed, 7, cidx) % np.uint64(1000)).astype(np.int64)
+    # grant bytes, certificate order: per op j the normal grant, then the faulty replica's variant
+    parts, pos = [], 0
+    off_norm = np.zeros((C, k), np.uint64)
+    len_norm = np.zeros((C, k), np.uint32)
+    off_var = np.zeros((C, k), np.uint64)
+    len_var = np.zeros((C, k), np.uint32)
+    expected = np.zeros((C, TXN_HASH_BYTES), np.uint8)
+    for i in range(C):
+        c = int(cidx[i])
+        th = hashlib.sha512(f"txn-{c}".encode()).hexdigest()
+        expected[i] = np.frombuffer(th.encode(), np.uint8)
+        ts = 1000 * (c % 64) + int(hts[i])
+        f = fault[i]
+        for j in range(k):
+            oid = f"DEMO_KEY_STRESS_TEST_{(c * k + j) % 200}"
+            g = encode_grant(oid, ts, th)
+            off_norm[i, j], len_norm[i, j] = pos, len(g)
+            parts.append(g)
+            pos += len(g)
+            if f == FAULT_TS or f == FAULT_G0_HASH or f == FAULT_G1_HASH:
+                v = encode_grant(oid, ts + 1, th) if f == FAULT_TS else \
+                    encode_grant(oid, ts, hashlib.sha512(f"txn-{c}-evil".encode()).hexdigest())
+                off_var[i, j], len_var[i, j] = pos, len(v)
+                parts.append(v)
+                pos += len(v)
+    blob = np.frombuffer(b"".join(parts), np.uint8).copy()
+    # grid [C, R, k] -> kept grants in (certificate, replica, op) order
+    shape = (C, R, k)
+    rr = np.arange(R)[None, :, None]
+    is_rf = np.broadcast_to(rr == rf[:, None, None], shape)
+    f3 = np.broadcast_to(fault[:, None, None], shape)
+    use_var = ((f3 == FAULT_TS) | (f3 == FAULT_G0_HASH) | (f3 == FAULT_G1_HASH)) & is_rf
+    keep = np.ones(shape, bool)
+    keep[(f3 == FAULT_DROP) & is_rf] = False
+    goff_g = np.where(use_var, off_var[:, None, :], off_norm[:, None, :])
+    glen_g = np.where(use_var, len_var[:, None, :], len_norm[:, None, :])
+    sel = keep.reshape(-1)
+    goff = np.broadcast_to(goff_g, shape).reshape(-1)[sel].astype(np.uint64)
+    glen = np.broadcast_to(glen_g, shape).reshape(-1)[sel].astype(np.uint32)
+    signer = np.broadcast_to(rr, shape).reshape(-1)[sel].astype(np.uint16)
+    gkey = np.broadcast_to(np.arange(k)[None, None, :], shape).reshape(-1)[sel].astype(np.uint8)
+    n = goff.shape[0]
+    sig = np.zeros((n, RSA_BYTES), np.uint8)
+    for r in range(R):
+        idx = np.nonzero(signer == r)[0]
+        s = mh.DeviceSigner(pems[r], device)
+        sig[idx] = s.sign(blob, goff[idx], glen[idx])
+        s.close()
+    per_cert = keep.reshape(C, -1).sum(1)
+    cert_grant_off = np.zeros(C + 1, np.uint32)
+    np.cumsum(per_cert, out=cert_grant_off[1:])
+    flags = np.full(n, 0x03, np.uint8)
+    flip_c = np.nonzero(fault == FAULT_FLIP)[0]
+    if flip_c.size:
+        gi = cert_grant_off[flip_c].astype(np.int64) + rf[flip_c] * k
+        bit = (_h(seed, 4, cidx[flip_c]) % np.uint64(2048)).astype(np.int64)
+        sig[gi, bit // 8] ^= (1 << (bit % 8)).astype(np.uint8)
+        flags[gi] = 0x02
+    batch = Batch(grant_bytes=blob, grant_off=goff, grant_len=glen, sig=sig, signer=signer, grant_key=gkey,
+                  cert_grant_off=cert_grant_off,
+                  cert_op_off=(np.arange(C + 1, dtype=np.uint64) * k).astype(np.uint32),
+                  op_key=np.tile(np.arange(k, dtype=np.uint8), C), op_flags=np.full(C * k, local_flags, np.uint8),
+                  expected_hash=expected)
+    return Synth(batch, np.zeros(C, np.int64), fault, rf, flags)
+
+
+def save_batch(path: str, s: Synth) -> None:
+    b = s.batch
+    np.savez(path, **{f: getattr(b, f) for f in ("grant_bytes", "grant_off", "grant_len", "sig", "signer",
+                                                  "grant_key", "cert_grant_off", "cert_op_off", "op_key",
+                                                  "op_flags", "expected_hash")},
+             fault=s.fault, fault_replica=s.fault_replica, expected_flags=s.expected_flags)
+
+
+def load_batch(path: str) -> Synth:
+    z = np.load(path)
+    b = Batch(**{f: z[f] for f in ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key",
+                                   "cert_grant_off", "cert_op_off", "op_key", "op_flags", "expected_hash")})
+    return Synth(b, np.zeros(b.n_certs, np.int64), z["fault"], z["fault_replica"], z["expected_flags"])
+
+
+def head_certs(s: Synth, n: int) -> Synth:
+    """The first n certificates of a synthetic batch (grant blob shared)."""
+    b = s.batch
+    n = max(0, min(n, b.n_certs))
+    g = int(b.cert_grant_off[n])
+    o = int(b.cert_op_off[n])
+    nb = Batch(grant_bytes=b.grant_bytes, grant_off=b.grant_off[:g], grant_len=b.grant_len[:g], sig=b.sig[:g],
+               signer=b.signer[:g], grant_key=b.grant_key[:g], cert_grant_off=b.cert_grant_off[:n + 1],
+               cert_op_off=b.cert_op_off[:n + 1], op_key=b.op_key[:o], op_flags=b.op_flags[:o],
+               expected_hash=b.expected_hash[:n])
+    return Synth(nb, s.template[:n], s.fault[:n], s.fault_replica[:n], s.expected_flags[:g])

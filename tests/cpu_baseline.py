@@ -36,23 +36,43 @@ def _work(rng):
     return b, e, flags[b:e].copy(), ts[b:e].copy()
 
 
-def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=None):
+def _wait_for(path, timeout_s=900):
+    t0 = time.time()
+    while not os.path.exists(path):
+        if time.time() - t0 > timeout_s:
+            raise TimeoutError(path)
+        time.sleep(0.2)
+
+
+def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=None, batch_file=None):
     import numpy as np
 
+    import mochi_hip as mh
     import oracle_ffi as O
     import workload as W
 
-    pool = W.build_pool(R=R, k=k, P=pool_size, P_f=256, cache_dir=cache_dir)
+    if batch_file:
+        # the bench's own stream (unique grants, signed on the GPU by the parent
+        # process); this process never touches the GPU
+        _wait_for(batch_file)
+        full = W.load_batch(batch_file)
+        moduli = [mh.pem_modulus(p) for p in W.load_keys(R)]
+        probe = W.head_certs(full, 256)
+        make = lambda n: W.head_certs(full, n)
+    else:
+        pool = W.build_pool(R=R, k=k, P=pool_size, P_f=256, cache_dir=cache_dir)
+        moduli = pool.moduli
+        probe = W.make_batch(pool, 256)
+        make = lambda n: W.make_batch(pool, n)
     # calibrate: one process, a few hundred grants
-    probe = W.make_batch(pool, 256)
     t0 = time.perf_counter()
-    O.verify_grants(pool.moduli, probe.batch, 0, probe.batch.n_grants, 1)
+    O.verify_grants(moduli, probe.batch, 0, probe.batch.n_grants, 1)
     rate1 = probe.batch.n_grants / max(1e-6, time.perf_counter() - t0)
     want = int(rate1 * procs * seconds / (R * k))
     n = max(64, min(n_certs, want))
-    s = W.make_batch(pool, n)
+    s = make(n)
     N = s.batch.n_grants
-    _G["moduli"], _G["batch"] = pool.moduli, s.batch.normalized()
+    _G["moduli"], _G["batch"] = moduli, s.batch.normalized()
     chunks = max(procs * 4, 1)
     ranges = [(N * i // chunks, N * (i + 1) // chunks) for i in range(chunks)]
     ctx = mp.get_context("fork")
@@ -82,9 +102,9 @@ def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=N
         "unit": "grants/s",
         "cores": procs,
         "kind": "port",
-        "sample": f"first {n} certificates ({N} grants) of the C2 stream; OpenSSL 3.0.2 SHA-256 + RSA-2048 PKCS#1 "
+        "sample": f"first {n} certificates ({N} grants) of the C2 stream{' (unique grants)' if batch_file else ''}; OpenSSL 3.0.2 SHA-256 + RSA-2048 PKCS#1 "
                   f"v1.5 verify per grant + restated InMemoryDataStore.java:576-640 tally; {procs} worker processes "
-                  f"on '{cpu}'; {dt:.1f} s",
+                  f"on '{cpu}'; {dt:.2f} s wall x {procs} processes = {dt * procs:.1f} core-seconds of CPU work",
         "single_core_grants_per_s": round(rate1, 1),
         "n_certs": n,
         "n_grants": N,
@@ -102,10 +122,11 @@ def main():
     ap.add_argument("--seconds", type=float, default=12.0)
     ap.add_argument("--client-predicate", action="store_true")
     ap.add_argument("--flags-out", default=None)
+    ap.add_argument("--batch-file", default=None, help="wait for and load this saved batch (bench's unique stream)")
     a = ap.parse_args()
     procs = a.procs or max(1, min(16, len(os.sched_getaffinity(0))))
     res = run(a.replication, a.ops_per_txn, a.pool, a.cache_dir, a.max_certs, procs, a.seconds,
-              not a.client_predicate, a.flags_out)
+              not a.client_predicate, a.flags_out, a.batch_file)
     print(json.dumps(res), flush=True)
 
 
