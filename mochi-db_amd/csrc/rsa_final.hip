@@ -51,6 +51,9 @@ __global__ __launch_bounds__(256, 2) void k_rsa_final(const uint32_t* __restrict
 #pragma unroll
   for (int j = 0; j < kL; j++) x[j] = zin[(size_t)j * n_slots + ws.slot];
   mont_mul<false>(x, x, nullptr, sv, n, n0inv);  // x = u
+  // keep the scalar loads of q / a2 below this point: hoisted above the
+  // multiply they would sit in SGPRs beside n's 74 limbs and spill
+  __asm__ volatile("" ::: "memory");
 
   // digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
   uint32_t hl[kHL];
