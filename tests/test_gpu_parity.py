@@ -185,6 +185,20 @@ def test_large_batch_c2_bit_exact(pool4, ver4):
     np.testing.assert_array_equal(g.grant_flags[:4000], of[:4000])
 
 
+@pytest.mark.parametrize("strict", [True, False])
+def test_large_batch_c3_bit_exact(pool7, ver7, strict):
+    """C3 scale (4M grants, R=7, both quorum predicates): flags vs ground truth,
+    verdicts / reasons / failing ops vs the oracle tally over the whole batch."""
+    C = W.n_certs_for_grants(4_000_000, 7)
+    s = W.make_batch(pool7, C)
+    g = ver7.verify(s.batch, 7, strict)
+    np.testing.assert_array_equal(g.grant_flags, s.expected_flags)
+    o = O.tally(s.batch, s.expected_flags, g.grant_ts, 7, strict)
+    np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits)
+    np.testing.assert_array_equal(g.cert_reason, o.cert_reason)
+    np.testing.assert_array_equal(g.cert_fail_op, o.cert_fail_op)
+
+
 def test_sig_ge_modulus_rejected(pool4, ver4):
     s = W.make_batch(pool4, 50, faults=False)
     b = s.batch
