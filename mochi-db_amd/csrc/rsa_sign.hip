@@ -12,11 +12,11 @@
 //   h  = qInv (m1 - m2) mod p,  s = m2 + h q  (Garner)
 //
 // PKCS#1 v1.5 signatures are deterministic, so s is bit-for-bit what OpenSSL's
-// EVP_DigestSign gives (tests/test_gpu_sign.py).  Exponentiation is left-to-
-// right square-and-multiply over the uniform exponent: ~1023 squarings +
-// ~512 multiplies per half, 2,072 / 2,738 v_mad_u64_u32 each (~7.0M per
-// signature).  Its time depends on the (public per-server, secret) exponent's
-// bit pattern, not on the message; see DESIGN.md for the side-channel note.
+// EVP_DigestSign gives (tests/test_gpu_sign.py).  Exponentiation is a fixed
+// 4-bit window over the uniform exponent: ~1,020 squarings + 255 multiplies +
+// 16 table products per half, 2,072 / 2,738 v_mad_u64_u32 each (~5.8M per
+// signature).  The operation sequence depends only on the exponent's length,
+// neither on the message nor on the exponent's bits.
 #include "../../include/mochi_hip.h"
 #include "kernels.h"
 #include "mont_crt.h"
@@ -37,15 +37,53 @@ struct SignKey {
 
 namespace {
 
+// Fixed 4-bit-window exponentiation: T[j] = base^j (Montgomery form, T[0] = R
+// mod p), then for every window below the top one 4 squarings and ONE
+// multiply by T[window] -- including window 0, so the operation sequence
+// depends only on the exponent's length, not on its bits.  ~1,020 squarings +
+// 255 multiplies + 16 table products per 1024-bit half, vs ~1,023 + ~512 for
+// square-and-multiply.  The window value is wave-uniform (one key per
+// launch), so T lives in per-lane private (scratch) memory indexed by a
+// uniform value: 37 coalesced scratch loads per multiply; the runtime sizes
+// scratch for the resident waves only.
 template <int L>
-__device__ __forceinline__ void mont_pow(uint32_t (&acc)[L], const uint32_t (&base)[L], cptr e, uint32_t ebits,
-                                         cptr n, uint32_t n0inv) {
+__device__ __forceinline__ void mont_pow(uint32_t (&acc)[L], const uint32_t (&base)[L], cptr r3, cptr e,
+                                         uint32_t ebits, cptr n, uint32_t n0inv) {
+  uint32_t tbl[16][L];
+  uint32_t t[L];
+  {
+    // T[0] = R mod p: MontMul(R^3, 1) = R^2, MontMul(R^2, 1) = R  (both < 2p)
+    uint32_t one[L] = {};
+    one[0] = 1;
+    const uint32_t unused[L] = {};
+    mont_mul_n<L, true>(t, one, r3, unused, n, n0inv);
+    mont_mul_n<L, false>(t, t, nullptr, one, n, n0inv);
+  }
 #pragma unroll
-  for (int j = 0; j < L; j++) acc[j] = base[j];  // the exponent's top bit
+  for (int j = 0; j < L; j++) {
+    tbl[0][j] = t[j];
+    tbl[1][j] = base[j];
+    t[j] = base[j];
+  }
 #pragma unroll 1
-  for (int i = (int)ebits - 2; i >= 0; i--) {
-    mont_sqr_n<L>(acc, n, n0inv);
-    if ((e[i >> 5] >> (i & 31)) & 1u) mont_mul_n<L, false>(acc, acc, nullptr, base, n, n0inv);
+  for (int w = 2; w < 16; w++) {
+    mont_mul_n<L, false>(t, t, nullptr, base, n, n0inv);
+#pragma unroll
+    for (int j = 0; j < L; j++) tbl[w][j] = t[j];
+  }
+  const int nwin = (int)(ebits + 3) >> 2;  // ebits >= 2
+  auto window = [&](int i) -> uint32_t { return (e[i >> 3] >> ((i & 7) * 4)) & 15u; };
+  const uint32_t top = window(nwin - 1);  // != 0: the exponent's top bit lies in it
+#pragma unroll
+  for (int j = 0; j < L; j++) acc[j] = tbl[top][j];
+#pragma unroll 1
+  for (int i = nwin - 2; i >= 0; i--) {
+#pragma unroll 1
+    for (int s = 0; s < 4; s++) mont_sqr_n<L>(acc, n, n0inv);
+    const uint32_t w = window(i);
+#pragma unroll
+    for (int j = 0; j < L; j++) t[j] = tbl[w][j];
+    mont_mul_n<L, false>(acc, acc, nullptr, t, n, n0inv);
   }
 }
 
@@ -61,7 +99,7 @@ __device__ __forceinline__ void crt_half(uint32_t (&out)[kLh], const uint32_t (&
   }, pr, p0inv);
   const uint32_t unused[kLh] = {};
   mont_mul_n<kLh, true>(base, base, r3, unused, pr, p0inv);  // EM * R (Montgomery form)
-  mont_pow<kLh>(acc, base, d, dbits, pr, p0inv);
+  mont_pow<kLh>(acc, base, r3, d, dbits, pr, p0inv);
   redc_wide<kLh>(out, [&](auto kc) -> uint64_t {  // out of Montgomery form
     constexpr int k = decltype(kc)::value;
     if constexpr (k < kLh) return acc[k];
