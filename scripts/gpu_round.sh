@@ -9,6 +9,6 @@ tail -3 $OUT/pytest_gpu.log
 timeout -k 10 400 python bench.py --steps 10 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof_kt" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --headline-only > "$R/$OUT/prof_kt.log" 2>&1 || { tail -20 "$R/$OUT/prof_kt.log"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof_kt" -o run -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --headline-only > "$R/$OUT/prof_kt.log" 2>&1 || { tail -20 "$R/$OUT/prof_kt.log"; exit 1; }
 find "$R/$OUT/prof_kt" -name "*stats*" | head
 timeout -k 10 120 rocprofv3 -L > "$R/$OUT/counters.txt" 2>&1 || true
