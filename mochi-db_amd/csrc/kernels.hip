@@ -55,11 +55,40 @@ __global__ __launch_bounds__(256) void k_grant_prep(const uint8_t* __restrict__ 
 // ---------------------------------------------------------------------------
 // Signer buckets (64-aligned) — counting sort.
 // ---------------------------------------------------------------------------
+// Wave-aggregated LDS counter add: the lanes of a wave that share a key are
+// ranked by ballot and their leader adds the group's size once, so a batch
+// with few signers (R = 4) costs a handful of LDS atomics per wave instead of
+// 64 same-address ones.  Returns this lane's slot (base + rank in the wave);
+// lanes with key == 0xFFFFFFFF take no part.  Must be reached by the whole wave.
+__device__ __forceinline__ uint32_t wave_counted_add(uint32_t* __restrict__ lcount, uint32_t key) {
+  bool pending = key != 0xFFFFFFFFu;
+  uint32_t slot = 0;
+  while (true) {
+    const uint64_t pm = __ballot(pending);
+    if (pm == 0) break;
+    const int leader = __ffsll((unsigned long long)pm) - 1;
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);  // scalar, no LDS round trip
+    const bool mine = pending && key == k;
+    const uint64_t mm = __ballot(mine);
+    uint32_t base = 0;
+    if ((int)__lane_id() == leader) base = atomicAdd(&lcount[k], (uint32_t)__popcll(mm));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    if (mine) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+      slot = base + below;
+      pending = false;
+    }
+  }
+  return slot;
+}
+
 __global__ __launch_bounds__(256) void k_bucket_count(const uint16_t* __restrict__ signer, uint32_t n, uint32_t n_keys,
                                                       uint32_t* __restrict__ count) {
   extern __shared__ uint32_t hist[];
   for (uint32_t k = threadIdx.x; k < n_keys; k += blockDim.x) hist[k] = 0;
   __syncthreads();
+  // no-return LDS atomics pipeline; the wave-aggregated form (wave_counted_add)
+  // measured 65 us vs 17 us here at C2
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t s = signer[i];
     if (s < n_keys) atomicAdd(&hist[s], 1u);
@@ -96,6 +125,11 @@ __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t* __restrict_
   }
 }
 
+// Each block places kScatterPer x 256 grants: ranks within the block come from
+// wave_counted_add, then ONE global cursor add per (block, signer) — 489
+// blocks x R adds at C2 instead of 3,906 x R.
+constexpr uint32_t kScatterPer = 8;
+
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint16_t* __restrict__ signer, uint32_t n, uint32_t n_keys,
                                                         uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm) {
   extern __shared__ uint32_t lds[];  // [n_keys] local count, then [n_keys] base
@@ -103,18 +137,23 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint16_t* __restri
   uint32_t* lbase = lds + n_keys;
   for (uint32_t k = threadIdx.x; k < n_keys; k += blockDim.x) lcount[k] = 0;
   __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t s = 0xFFFFFFFFu, rank = 0;
-  if (i < n) {
-    s = signer[i];
-    if (s < n_keys) rank = atomicAdd(&lcount[s], 1u);
-    else s = 0xFFFFFFFFu;
+  const uint32_t i0 = blockIdx.x * (blockDim.x * kScatterPer) + threadIdx.x;
+  uint32_t s[kScatterPer], rank[kScatterPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kScatterPer; j++) {
+    const uint32_t i = i0 + j * blockDim.x;
+    uint32_t v = i < n ? (uint32_t)signer[i] : 0xFFFFFFFFu;
+    s[j] = v < n_keys ? v : 0xFFFFFFFFu;
   }
+#pragma unroll
+  for (uint32_t j = 0; j < kScatterPer; j++) rank[j] = wave_counted_add(lcount, s[j]);
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < n_keys; k += blockDim.x)
     lbase[k] = lcount[k] ? atomicAdd(&cursor[k], lcount[k]) : 0u;
   __syncthreads();
-  if (s != 0xFFFFFFFFu) perm[lbase[s] + rank] = i;
+#pragma unroll
+  for (uint32_t j = 0; j < kScatterPer; j++)
+    if (s[j] != 0xFFFFFFFFu) perm[lbase[s[j]] + rank[j]] = i0 + j * blockDim.x;
 }
 
 // ---------------------------------------------------------------------------
@@ -252,11 +291,27 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     if (a.prof_events) (void)hipEventRecord(a.prof_events[2 * stage + (end ? 1 : 0)], s);
   };
   // grant prep (parse + SHA-256) only feeds k_rsa_final and k_tally, so it runs
-  // beside bucketing + k_rsa_pow on the aux stream and fills their idle issue
-  // slots (it is latency-bound); the launch stream joins it before k_rsa_final
+  // beside k_rsa_pow on the aux stream and fills its idle issue slots (it is
+  // latency-bound); the launch stream joins it before k_rsa_final.  It forks
+  // AFTER bucketing: run beside prep, the short bucket kernels (which gate
+  // k_rsa_pow) took ~4x longer
   const bool prep = N && !a.skip_prep_tally;
   const bool fork = prep && a.aux;
   hipStream_t ps = fork ? a.aux : st;
+  mark(kStageBucket, false, st);
+  if (N) {
+    hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, st);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(a.perm, 0xFF, sizeof(uint32_t) * (size_t)a.n_slots, st);
+    if (e != hipSuccess) return e;
+    const uint32_t lds = sizeof(uint32_t) * a.n_keys;
+    const uint32_t cblocks = cdiv(N, 256) < 1024 ? cdiv(N, 256) : 1024;
+    hipLaunchKernelGGL(k_bucket_count, dim3(cblocks), dim3(256), lds, st, a.signer, N, a.n_keys, a.count);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, a.count, a.n_keys, a.cursor, a.total);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(cdiv(N, 256 * kScatterPer)), dim3(256), 2 * lds, st, a.signer, N, a.n_keys, a.cursor,
+                       a.perm);
+  }
+  mark(kStageBucket, true, st);
   if (fork) {
     hipError_t e = hipEventRecord(a.ev_fork, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(a.aux, a.ev_fork, 0);
@@ -271,20 +326,6 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     hipError_t e = hipEventRecord(a.ev_join, a.aux);
     if (e != hipSuccess) return e;
   }
-  mark(kStageBucket, false, st);
-  if (N) {
-    hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, st);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(a.perm, 0xFF, sizeof(uint32_t) * (size_t)a.n_slots, st);
-    if (e != hipSuccess) return e;
-    const uint32_t lds = sizeof(uint32_t) * a.n_keys;
-    const uint32_t cblocks = cdiv(N, 256) < 1024 ? cdiv(N, 256) : 1024;
-    hipLaunchKernelGGL(k_bucket_count, dim3(cblocks), dim3(256), lds, st, a.signer, N, a.n_keys, a.count);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, a.count, a.n_keys, a.cursor, a.total);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(cdiv(N, 256)), dim3(256), 2 * lds, st, a.signer, N, a.n_keys, a.cursor,
-                       a.perm);
-  }
-  mark(kStageBucket, true, st);
   mark(kStagePow, false, st);
   if (N) launch_rsa_pow(a, st);
   mark(kStagePow, true, st);
