@@ -169,7 +169,7 @@ struct mochi_ctx {
   DevBuf dev_in, dev_out;
   PinnedBuf pin_in, pin_out;
   hipStream_t s_in = nullptr, s_out = nullptr;  // host-path copy streams
-  hipStream_t aux = nullptr;                     // grant prep, overlapped with bucketing + k_rsa_pow
+  hipStream_t aux = nullptr;                     // grant prep (high priority), overlapped with k_rsa_pow
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<hipEvent_t> chunk_ev;              // host-path chunk hand-offs
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -197,6 +197,17 @@ int mochi_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+// The grant-prep stream runs at the highest priority: its short latency-bound
+// kernel is dispatched ahead of the k_rsa_pow blocks it overlaps, finishes
+// early and hands the CUs back, instead of trickling beside pow for the whole
+// launch (and taking VGPR slots from it).
+static hipError_t create_prep_stream(hipStream_t* s) {
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
 mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_keys, uint32_t key_bytes,
@@ -238,7 +249,7 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
   (void)hipGetDevice(&save);
   bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
+            create_prep_stream(&c->aux) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) == hipSuccess &&
             hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) == hipSuccess &&
