@@ -92,6 +92,36 @@ def test_rsa_public_op_matches_python_pow():
     ver.close()
 
 
+@pytest.mark.parametrize("layout", ["shuffled", "skewed"])
+def test_bucketing_many_signers(layout):
+    """Signer bucketing (k_bucket_count/scan/scatter) at MOCHI_MAX_KEYS = 4096 keys:
+    waves holding up to 64 distinct signers (wave-aggregated ranking loops once
+    per distinct key) and a skewed mix where one key takes most grants.  The
+    moduli are random odd 2048-bit integers (Montgomery needs only gcd(R, n) = 1);
+    every lane's s^65537 mod n is checked against Python's pow."""
+    rng = np.random.default_rng(11 if layout == "shuffled" else 12)
+    n_keys = 4096
+    mods = []
+    for _ in range(n_keys):
+        v = int.from_bytes(rng.bytes(256), "big") | (3 << 2046) | 1
+        mods.append(v.to_bytes(256, "big"))
+    ver = mh.Verifier(mods, 0)
+    n = 20000
+    if layout == "shuffled":
+        signer = rng.integers(0, n_keys, n)
+    else:
+        signer = np.where(rng.random(n) < 0.9, 17, rng.integers(0, n_keys, n))
+    sigs = []
+    for k in signer:
+        N = int.from_bytes(mods[k], "big")
+        sigs.append((int.from_bytes(rng.bytes(256), "big") % N).to_bytes(256, "big"))
+    y = mh.rsa_public_op(ver, np.frombuffer(b"".join(sigs), np.uint8), signer.astype(np.uint16))
+    for i in range(n):
+        N = int.from_bytes(mods[signer[i]], "big")
+        assert int.from_bytes(y[i].tobytes(), "big") == pow(int.from_bytes(sigs[i], "big"), 65537, N), i
+    ver.close()
+
+
 def test_rsa_golden_vectors_gpu(golden_dir):
     d = json.load(open(os.path.join(golden_dir, "rsa_vectors.json")))
     moduli = [bytes.fromhex(d["moduli"][str(i)]) for i in range(7)]
