@@ -125,6 +125,7 @@ def main():
     N = batch.n_grants
 
     ver = mh.Verifier(moduli, device=local_rank)
+    ver.moduli = moduli  # for the second context of the pipelined wire leg
     dev = mh.DeviceBatch(batch, local_rank)
     out = mh.DeviceVerdicts(dev.n_grants, dev.n_certs, local_rank, full=True)
     stream = torch.cuda.current_stream()
@@ -310,10 +311,68 @@ def wire_path(ver, pool, synth, R, strict, dev, stream, args):
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / args.steps
     N = synth.batch.n_grants
+    pipe = wire_pipelined(ver, dwb, R, strict, dev, args, N, host)
     return {"grants_per_s": round(N / t, 1), "ms_per_step": round(t * 1e3, 4), "messages": wb.n_msgs,
             "wire_bytes": int(wb.wire.nbytes), "verdicts_equal_soa_path": same,
             "host_encode_s": round(enc_s, 2),
-            "note": "Write2ToServer bodies resident in HBM; includes one host wait on the decoded totals per step"}
+            "note": "Write2ToServer bodies resident in HBM; includes one host wait on the decoded totals per step",
+            "pipelined_2ctx": pipe}
+
+
+def wire_pipelined(ver, dwb, R, strict, dev, args, N, ref_host):
+    """Two batches in flight: a second context (own streams and scratch) driven by a
+    second host thread, so one batch's latency-bound decode runs beside the other's
+    k_rsa_pow -- how a server keeps the GPU busy with back-to-back batches (the
+    batcher's next batch accumulates while one is on the GPU).  Wall-clock over
+    2 x steps batches, both streams synchronised on both sides."""
+    import copy
+    import threading
+
+    import numpy as np
+    import torch
+
+    import mochi_hip as mh
+    import workload as W
+
+    ver_b = mh.Verifier(ver.moduli, device=dev)
+    ver_b.set_server_ids(W.SERVER_IDS[:R])
+    dwb_b = copy.copy(dwb)  # same read-only wire bytes, own status array
+    dwb_b.status = torch.zeros_like(dwb.status)
+    lanes = [(ver, dwb, torch.cuda.Stream(dev)), (ver_b, dwb_b, torch.cuda.Stream(dev))]
+    outs = [mh.DeviceVerdicts(0, dwb.n_msgs, dev, full=True) for _ in lanes]
+    for o in outs:
+        o.grant_flags = o.grant_ts = None
+    errs = []
+
+    def run(i, n):
+        v, d, st = lanes[i]
+        try:
+            for _ in range(n):
+                v.verify_write2_device(d, outs[i], R, strict, stream=st.cuda_stream)
+            st.synchronize()
+        except Exception as e:  # surfaced after join
+            errs.append(e)
+
+    def both(n):
+        th = [threading.Thread(target=run, args=(i, n)) for i in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if errs:
+            raise errs[0]
+
+    both(max(1, args.warmup))
+    same = all(np.array_equal(o.to_host().cert_reason, ref_host.cert_reason) for o in outs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    both(args.steps)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ver_b.close()
+    t = wall / (2 * args.steps)
+    return {"grants_per_s": round(N / t, 1), "ms_per_batch": round(t * 1e3, 4), "contexts": 2,
+            "batches": 2 * args.steps, "verdicts_equal": bool(same), "timing": "host wall clock"}
 
 
 def sign_path(pem, batch, dev, stream, args, n_gpu=262144, n_cpu=16384):
