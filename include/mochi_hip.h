@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MOCHI_ABI_VERSION 1
+#define MOCHI_ABI_VERSION 2
 #define MOCHI_RSA_BYTES 256     /* RSA-2048 modulus / signature size            */
 #define MOCHI_RSA_E 65537u      /* the only public exponent supported          */
 #define MOCHI_TXN_HASH_BYTES 128 /* lowercase-hex SHA-512 (Utils.java:135-153)  */
@@ -72,13 +72,50 @@ enum mochi_reason {
   MOCHI_REJECT_MALFORMED = 6,
   /* Write2 wire path only: the message is legal protobuf but outside the
    * device decoder's fast path (enum mochi_msg_status MOCHI_MSG_FALLBACK /
-   * MOCHI_MSG_OPS_MISMATCH); not accepted here, verify it on the host path. */
+   * MOCHI_MSG_OPS_MISMATCH) and the library's host decoder could not decide it
+   * either (more than MOCHI_MAX_OPS_PER_CERT operations, or op_flags_off giving a
+   * different operation count).  Never accepted. */
   MOCHI_UNDECIDED = 7,
+  /* applyOperation: setCurrentC(wc) then getCurrentTimestampFromCurrentCertificate()
+   * on the INCOMING certificate (InMemoryDataStore.java:533-534) throws
+   * IllegalStateException: some MultiGrant of the certificate has no grant for the
+   * op's key (StoreValueObjectContainer.java:186, Utils.assertNotNull) or two of
+   * them carry different timestamps (:192-194).  Every MultiGrant counts here,
+   * whatever its signatures (the Java loop runs over the stored certificate as
+   * received).  Side effect in the reference: currentC is already replaced. */
+  MOCHI_REJECT_APPLY_STATE = 8,
+  /* write2apply :594: the key's STORED currentC throws in
+   * getCurrentTimestampFromCurrentCertificate (op flag MOCHI_OP_CURRENT_C_BAD) ->
+   * IllegalStateException. */
+  MOCHI_REJECT_STORED_CERT = 9,
+  /* readOperation / applyOperation on an op that is not a WRITE/DELETE, or whose
+   * key holds no write lock (empty operand1 is never locked,
+   * InMemoryDataStore.java:339-358): IllegalStateException (:525-526 / :560-561)
+   * or UnsupportedOperationException (:551 / :572).  Op flag MOCHI_OP_NOT_WRITE. */
+  MOCHI_REJECT_NOT_WRITE = 10,
+};
+
+/* Per-operation outcome of write2apply's loop (InMemoryDataStore.java:581-609),
+ * mochi_verdicts.op_decision.  The reference is not atomic: the ops before a
+ * failing op have already been applied when it throws. */
+enum mochi_op_decision {
+  MOCHI_OPD_SKIPPED = 0,     /* not reached (the certificate was rejected earlier)        */
+  MOCHI_OPD_APPLY = 1,       /* applyOperation(op, wc) (:597): currentC := wc, ts = op_ts  */
+  MOCHI_OPD_READ = 2,        /* readOperation(op) (:596): objectTS > g0.timestamp          */
+  MOCHI_OPD_WRONG_SHARD = 3, /* WRONG_SHARD result (:582-587)                              */
+  MOCHI_OPD_FAILED = 4,      /* this op's step threw: cert_reason / cert_fail_op          */
 };
 
 /* op_flags bits (one byte per transaction operation). */
 #define MOCHI_OP_LOCAL 0x01    /* objectBelongsToCurrentShardServer(key)      InMemoryDataStore.java:63-72,582 */
 #define MOCHI_OP_HAS_SVOC 0x02 /* getDataMap(key).get(key) != null           InMemoryDataStore.java:592 */
+#define MOCHI_OP_HAS_CURRENT_C 0x04 /* the SVOC holds a certificate (currentC != null); its timestamp,
+                                       getCurrentTimestampFromCurrentCertificate(), is op_object_ts[o]
+                                       (StoreValueObjectContainer.java:175-198, InMemoryDataStore.java:594) */
+#define MOCHI_OP_CURRENT_C_BAD 0x08 /* the SVOC's stored currentC makes that call throw (:594)    */
+#define MOCHI_OP_NOT_WRITE 0x10     /* action is not WRITE/DELETE, or operand1 is empty (no write
+                                       lock): the read/apply step throws.  The wire decoder sets it
+                                       itself from Operation.action / operand1. */
 
 /* grant_flags bits (one byte per grant, output). */
 #define MOCHI_GRANT_SIG_OK 0x01   /* RSA/SHA-256 signature verified            */
@@ -101,7 +138,7 @@ typedef struct mochi_batch {
   uint32_t n_grants;              /* N */
   uint32_t n_certs;               /* C */
   uint32_t n_ops;                 /* O = total transaction operations over all certificates */
-  uint32_t _pad0;
+  uint32_t n_mgs;                 /* total MultiGrants (size of mg_grant_off - 1); 0 with cert_mg_off NULL */
   uint64_t grant_bytes_len;       /* size of grant_bytes                                      */
   const uint8_t* grant_bytes;     /* blob holding every grant's proto3 bytes                  */
   const uint64_t* grant_off;      /* [N] byte offset of grant i in grant_bytes                */
@@ -114,13 +151,41 @@ typedef struct mochi_batch {
   const uint8_t* op_key;          /* [O] key slot of each op (ops on the same key share a slot) */
   const uint8_t* op_flags;        /* [O] MOCHI_OP_* bits                                        */
   const uint8_t* expected_hash;   /* [C * 128] objectSHA512(txn) as lowercase hex (host-computed, §7.1.4) */
+  /* --- ABI 2 --- */
+  /* MultiGrant boundaries (the certificate map's values, wire order): the
+   * MultiGrants of cert c are [cert_mg_off[c], cert_mg_off[c+1]) and the grants of
+   * MultiGrant m are [mg_grant_off[m], mg_grant_off[m+1]) (empty MultiGrants
+   * allowed); mg_grant_off[cert_mg_off[c]] == cert_grant_off[c].  NULL: every
+   * maximal run of consecutive grants with one signer is one MultiGrant. */
+  const uint32_t* cert_mg_off;    /* [C+1] or NULL                                              */
+  const uint32_t* mg_grant_off;   /* [n_mgs+1] or NULL                                          */
+  const int64_t* op_object_ts;    /* [O] stored currentC timestamp, read iff MOCHI_OP_HAS_CURRENT_C; NULL = none */
+  /* The op key (Operation.operand1) bytes, as a slice of grant_bytes: needed only
+   * by MOCHI_Q_BIND (Grant.objectId must equal it).  NULL otherwise. */
+  const uint64_t* op_key_off;     /* [O] offset in grant_bytes                                  */
+  const uint32_t* op_key_len;     /* [O]                                                        */
 } mochi_batch;
+
+/* mochi_params.quorum_mode bits.  0 = parity with the reference: every
+ * signature-valid grant of the certificate counts once per op naming its key
+ * (InMemoryDataStore.java:613-640, :590), whoever signed it.  The bits make the
+ * new signature layer a Byzantine quorum; a grant they exclude is treated like
+ * one with an invalid signature (absent, :622-624). */
+#define MOCHI_Q_DISTINCT_SIGNERS 0x1 /* a signer counts at most once per key: only its first valid
+                                        grant for the key (wire order) counts.  The honest client keys
+                                        the certificate by MultiGrant.serverId (MochiDBClient.java:299,
+                                        334), so honest certificates are unaffected. */
+#define MOCHI_Q_BIND 0x2             /* a grant counts only if Grant.objectId equals the op key it is
+                                        filed under and Grant.transactionHash equals expected_hash
+                                        (no replay of a signer's grants for other objects or
+                                        transactions).  Needs op_key_off / op_key_len. */
 
 typedef struct mochi_params {
   uint32_t replication_factor; /* R = _CONFIG_BFT_REPLICATION; majority M = 2*(R/3)+1 */
   uint32_t strict_gt;          /* 1: server predicate count > M (InMemoryDataStore.java:590)
                                   0: client predicate count >= M (MochiDBClient.java:172,379) */
-  uint32_t _pad[2];
+  uint32_t quorum_mode;        /* MOCHI_Q_* bits, 0 = reference parity */
+  uint32_t _pad;
 } mochi_params;
 
 typedef struct mochi_verdicts {
@@ -130,6 +195,11 @@ typedef struct mochi_verdicts {
   uint32_t* cert_accept_bits; /* [ceil(C/32)] bit c = certificate accepted       (required)    */
   uint8_t* cert_reason;       /* [C] enum mochi_reason                           (may be NULL) */
   uint8_t* cert_fail_op;      /* [C] op index of the first failing op, 0xFF if none / n.a. (may be NULL) */
+  /* --- ABI 2: per operation, in the batch's op order (may be NULL) --- */
+  uint8_t* op_decision;       /* [O] enum mochi_op_decision                                     */
+  uint32_t* op_g0;            /* [O] g0 of the op's key: certificate-relative index of the first
+                                 counted grant for it (InMemoryDataStore.java:588), 0xFFFFFFFF none */
+  int64_t* op_ts;             /* [O] g0's timestamp (the ts applyOperation records), 0 if none   */
 } mochi_verdicts;
 
 typedef struct mochi_ctx mochi_ctx;
@@ -327,6 +397,9 @@ typedef struct mochi_write2_batch {
   const uint32_t* op_flags_off;   /* [M+1] CSR into op_flags; NULL = every op LOCAL|HAS_SVOC    */
   const uint8_t* op_flags;        /* MOCHI_OP_* per operation, transaction order               */
   const uint8_t* expected_hash;   /* [M * 128] objectSHA512(transaction), lowercase hex         */
+  /* --- ABI 2 --- */
+  const int64_t* op_object_ts;    /* aligned with op_flags (CSR op_flags_off): stored currentC
+                                     timestamp, read iff MOCHI_OP_HAS_CURRENT_C; NULL = none      */
 } mochi_write2_batch;
 
 /* Server-id table of the context: key i of the key table belongs to the server
@@ -335,8 +408,17 @@ typedef struct mochi_write2_batch {
 int mochi_ctx_set_server_ids(mochi_ctx* ctx, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids);
 
 /* Decode + verify M Write2ToServer messages held in HOST memory.  Only the
- * certificate-level verdict arrays of `out` are written (grant-level pointers
- * must be NULL); msg_status[M] receives enum mochi_msg_status.  Synchronous. */
+ * certificate-level and per-op verdict arrays of `out` are written (grant-level
+ * pointers must be NULL); per-op arrays need op_flags_off and follow its layout
+ * (ops of messages that were not decoded read MOCHI_OPD_SKIPPED).
+ * msg_status[M] receives enum mochi_msg_status.  Messages the device decoder
+ * leaves to the host (MOCHI_MSG_FALLBACK: repeated / merged fields, non-canonical
+ * Grant bytes, more than 32 MultiGrants or 64 grants per MultiGrant) are decoded
+ * by the library's host decoder with full protobuf-java semantics and verified
+ * on the device like any other certificate -- signatures are always checked;
+ * msg_status still reports MOCHI_MSG_FALLBACK for them.  Synchronous; batches
+ * larger than the chunk target are pipelined (upload / decode+verify / download
+ * of consecutive chunks overlap). */
 int mochi_verify_write2(mochi_ctx* ctx, const mochi_write2_batch* batch, const mochi_params* params,
                         mochi_verdicts* out, uint8_t* msg_status);
 
@@ -351,7 +433,7 @@ int mochi_verify_write2_device(mochi_ctx* ctx, const mochi_write2_batch* batch, 
  * the library; release them with mochi_write2_decoded_free.  grant_off is
  * relative to the start of `wire`. */
 typedef struct mochi_write2_decoded {
-  uint32_t n_msgs, n_grants, n_ops, _pad0;
+  uint32_t n_msgs, n_grants, n_ops, n_mgs;
   uint64_t* grant_off;      /* [N] */
   uint32_t* grant_len;      /* [N] */
   uint8_t* sig;             /* [N * 256] */
@@ -362,6 +444,11 @@ typedef struct mochi_write2_decoded {
   uint8_t* op_key;          /* [O] */
   uint8_t* op_flags;        /* [O] */
   uint8_t* msg_status;      /* [M] enum mochi_msg_status */
+  /* ABI 2 */
+  uint32_t* cert_mg_off;    /* [M+1] MultiGrants per message (CSR) */
+  uint32_t* mg_grant_off;   /* [n_mgs+1] grants per MultiGrant (CSR) */
+  uint64_t* op_key_off;     /* [O] Operation.operand1, offset relative to `wire` */
+  uint32_t* op_key_len;     /* [O] */
 } mochi_write2_decoded;
 int mochi_write2_decode(mochi_ctx* ctx, const mochi_write2_batch* batch, mochi_write2_decoded* out);
 void mochi_write2_decoded_free(mochi_write2_decoded* d);

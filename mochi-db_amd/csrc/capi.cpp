@@ -171,7 +171,14 @@ struct mochi_ctx {
   hipStream_t s_in = nullptr, s_out = nullptr;  // host-path copy streams
   hipStream_t aux = nullptr;                     // grant prep (high priority), overlapped with k_rsa_pow
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // Scratch ordering: every launch that uses the context's scratch waits for
+  // the previous one to be done with it (the device entry points are async on a
+  // caller-chosen stream, so two calls on different streams would otherwise
+  // race on digest / perm / xbuf / decode buffers).
+  hipEvent_t ev_scratch = nullptr;
+  bool scratch_used = false;
   std::vector<hipEvent_t> chunk_ev;              // host-path chunk hand-offs
+  std::vector<hipEvent_t> tot_ev;                // wire host path: per-chunk decode totals on the host
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float last_ms[3] = {0, 0, 0};  // first upload, compute span, last download of the last host-path call
   float last_total_ms = 0;       // whole pipelined host-path call (first H2D start -> last D2H end)
@@ -179,9 +186,10 @@ struct mochi_ctx {
   // Write2 wire path: server-id table + decode scratch
   DevBuf ids, id_off;
   uint32_t n_ids = 0;
-  DevBuf w2_cnt_g, w2_cnt_o, w2_status, w2_scan, w2_cg, w2_co, w2_goff, w2_glen, w2_sig, w2_signer, w2_gkey,
-      w2_okey, w2_oflags, w2_sigsrc;
+  DevBuf w2_cnt, w2_status, w2_scan, w2_goff, w2_glen, w2_sig, w2_signer, w2_gkey, w2_okey, w2_oflags, w2_sigsrc,
+      w2_mgo, w2_ots, w2_okoff, w2_oklen;
   PinnedBuf w2_tot;
+  hipEvent_t ev_tot = nullptr;
   // per-stage profiling (mochi_ctx_set_profiling): one event set per verify call
   bool profiling = false;
   std::vector<std::vector<hipEvent_t>> prof_sets;
@@ -252,6 +260,8 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
             create_prep_stream(&c->aux) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_scratch, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming) == hipSuccess &&
             hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_keys, sizeof(mochi::KeyEntry) * n_keys) == hipSuccess &&
             hipMemcpy(c->d_keys, table.data(), sizeof(mochi::KeyEntry) * n_keys, hipMemcpyHostToDevice) == hipSuccess;
@@ -275,11 +285,14 @@ void mochi_ctx_destroy(mochi_ctx* c) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->chunk_ev) (void)hipEventDestroy(e);
+  for (auto& e : c->tot_ev) (void)hipEventDestroy(e);
   if (c->aux) (void)hipStreamSynchronize(c->aux);
   if (c->s_in) (void)hipStreamDestroy(c->s_in);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->ev_scratch) (void)hipEventDestroy(c->ev_scratch);
+  if (c->ev_tot) (void)hipEventDestroy(c->ev_tot);
   if (c->s_out) (void)hipStreamDestroy(c->s_out);
   if (c->d_keys) (void)hipFree(c->d_keys);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -300,6 +313,13 @@ int check_batch_header(const mochi_ctx* c, const mochi_batch* b, const mochi_par
   if (!b->cert_grant_off || !b->cert_op_off) return fail(MOCHI_EINVAL, "cert_grant_off / cert_op_off required");
   if (b->n_certs && !b->expected_hash) return fail(MOCHI_EINVAL, "expected_hash required");
   if (b->n_ops && (!b->op_key || !b->op_flags)) return fail(MOCHI_EINVAL, "op arrays required");
+  if ((b->cert_mg_off == nullptr) != (b->mg_grant_off == nullptr))
+    return fail(MOCHI_EINVAL, "cert_mg_off and mg_grant_off go together");
+  if (!b->cert_mg_off && b->n_mgs) return fail(MOCHI_EINVAL, "n_mgs must be 0 without cert_mg_off");
+  if ((p->quorum_mode & MOCHI_Q_BIND) && b->n_ops && (!b->op_key_off || !b->op_key_len))
+    return fail(MOCHI_EINVAL, "MOCHI_Q_BIND needs op_key_off / op_key_len");
+  if (p->quorum_mode & ~(uint32_t)(MOCHI_Q_DISTINCT_SIGNERS | MOCHI_Q_BIND))
+    return fail(MOCHI_EINVAL, "unknown quorum_mode bits 0x%x", p->quorum_mode);
   return MOCHI_OK;
 }
 
@@ -320,12 +340,36 @@ int check_batch_host(const mochi_batch* b) {
     if (b->grant_off[i] > b->grant_bytes_len || b->grant_len[i] > b->grant_bytes_len - b->grant_off[i])
       return fail(MOCHI_EINVAL, "grant %u lies outside grant_bytes", i);
   }
-  for (uint32_t o = 0; o < b->n_ops; o++)
+  for (uint32_t o = 0; o < b->n_ops; o++) {
     if (b->op_key[o] >= MOCHI_MAX_OPS_PER_CERT) return fail(MOCHI_EINVAL, "op_key[%u] >= %d", o, MOCHI_MAX_OPS_PER_CERT);
+    if (b->op_key_off && (b->op_key_off[o] > b->grant_bytes_len || b->op_key_len[o] > b->grant_bytes_len - b->op_key_off[o]))
+      return fail(MOCHI_EINVAL, "op key %u lies outside grant_bytes", o);
+  }
+  if (b->cert_mg_off) {
+    if (b->cert_mg_off[0] != 0 || b->cert_mg_off[b->n_certs] != b->n_mgs)
+      return fail(MOCHI_EINVAL, "cert_mg_off must start at 0 and end at n_mgs");
+    if (b->mg_grant_off[0] != 0 || b->mg_grant_off[b->n_mgs] != b->n_grants)
+      return fail(MOCHI_EINVAL, "mg_grant_off must start at 0 and end at n_grants");
+    for (uint32_t m = 0; m < b->n_mgs; m++)
+      if (b->mg_grant_off[m + 1] < b->mg_grant_off[m]) return fail(MOCHI_EINVAL, "mg_grant_off decreases at %u", m);
+    for (uint32_t c = 0; c < b->n_certs; c++)
+      if (b->cert_mg_off[c + 1] < b->cert_mg_off[c] || b->mg_grant_off[b->cert_mg_off[c]] != b->cert_grant_off[c])
+        return fail(MOCHI_EINVAL, "MultiGrants of cert %u do not cover its grants", c);
+  }
   return MOCHI_OK;
 }
 
-int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o, hipStream_t st) {
+// Scratch ordering across calls and streams (see mochi_ctx::ev_scratch).
+hipError_t scratch_acquire(mochi_ctx* c, hipStream_t st) {
+  return c->scratch_used ? hipStreamWaitEvent(st, c->ev_scratch, 0) : hipSuccess;
+}
+hipError_t scratch_release(mochi_ctx* c, hipStream_t st) {
+  c->scratch_used = true;
+  return hipEventRecord(c->ev_scratch, st);
+}
+
+int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o, hipStream_t st,
+               const uint32_t* op_out_off = nullptr) {
   const uint32_t N = b->n_grants, C = b->n_certs;
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
   if (slots > 0xFFFFFFF0ull) return fail(MOCHI_EINVAL, "batch too large");
@@ -354,6 +398,12 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.op_key = b->op_key;
   a.op_flags = b->op_flags;
   a.expected_hash = b->expected_hash;
+  a.cert_mg_off = b->cert_mg_off;
+  a.mg_grant_off = b->mg_grant_off;
+  a.op_object_ts = b->op_object_ts;
+  a.op_key_off = b->op_key_off;
+  a.op_key_len = b->op_key_len;
+  a.quorum_mode = p->quorum_mode;
   const uint32_t R = p->replication_factor;
   a.majority = 2 * (R / 3) + 1;  // ClusterConfiguration.getServerMajority  ClusterConfiguration.java:264-267
   a.strict_gt = p->strict_gt ? 1 : 0;
@@ -372,6 +422,10 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.cert_accept_bits = o->cert_accept_bits;
   a.cert_reason = o->cert_reason;
   a.cert_fail_op = o->cert_fail_op;
+  a.op_decision = o->op_decision;
+  a.op_g0 = o->op_g0;
+  a.op_ts = o->op_ts;
+  a.op_out_off = op_out_off;
   a.aux = c->aux;
   a.ev_fork = c->ev_fork;
   a.ev_join = c->ev_join;
@@ -381,7 +435,9 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
     c->prof_sets.push_back(evs);
     a.prof_events = c->prof_sets.back().data();
   }
+  HIP_TRY(scratch_acquire(c, st));
   HIP_TRY(mochi::launch_verify(a, st));
+  HIP_TRY(scratch_release(c, st));
   return MOCHI_OK;
 }
 
@@ -439,13 +495,21 @@ int ensure_scratch(mochi_ctx* c, uint32_t N) {
   return MOCHI_OK;
 }
 
+// Input segments of one chunk, in mochi_batch order.  The CSR arrays (6, 7,
+// 11, 12) are rebased per chunk and therefore always staged.
+enum Seg {
+  kBlob, kGrantOff, kGrantLen, kSig, kSigner, kGrantKey, kCertGrantOff, kCertOpOff, kOpKey, kOpFlags, kExpHash,
+  kCertMgOff, kMgGrantOff, kOpObjTs, kOpKeyOff, kOpKeyLen, kNumSeg
+};
+
 int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o) {
-  const uint32_t N = b->n_grants, C = b->n_certs;
+  const uint32_t N = b->n_grants, C = b->n_certs, O = b->n_ops;
+  const bool mg = b->cert_mg_off != nullptr;
   // --- plan chunks ---
   struct Chunk {
-    uint32_t c0, c1, g0, g1, o0, o1;
-    uint64_t lo, hi;  // grant byte range [lo, hi) in grant_bytes
-    size_t seg[11];   // device/staging offsets of the 11 input segments
+    uint32_t c0, c1, g0, g1, o0, o1, m0, m1;
+    uint64_t lo, hi;  // byte range [lo, hi) of grant_bytes this chunk reads
+    size_t seg[kNumSeg];
   };
   std::vector<Chunk> ch;
   uint32_t max_grants = 0;
@@ -460,52 +524,69 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
     k.g1 = b->cert_grant_off[c1];
     k.o0 = b->cert_op_off[c0];
     k.o1 = b->cert_op_off[c1];
+    k.m0 = mg ? b->cert_mg_off[c0] : 0;
+    k.m1 = mg ? b->cert_mg_off[c1] : 0;
     uint64_t lo = UINT64_MAX, hi = 0;
     for (uint32_t g = k.g0; g < k.g1; g++) {
       lo = b->grant_off[g] < lo ? b->grant_off[g] : lo;
       const uint64_t e = b->grant_off[g] + b->grant_len[g];
       hi = e > hi ? e : hi;
     }
-    k.lo = k.g1 > k.g0 ? lo : 0;
-    k.hi = k.g1 > k.g0 ? hi : 0;
+    if (b->op_key_off)  // MOCHI_Q_BIND reads the op keys from the blob too
+      for (uint32_t x = k.o0; x < k.o1; x++) {
+        lo = b->op_key_off[x] < lo ? b->op_key_off[x] : lo;
+        const uint64_t e = b->op_key_off[x] + b->op_key_len[x];
+        hi = e > hi ? e : hi;
+      }
+    if (lo == UINT64_MAX) lo = hi = 0;  // nothing read from the blob
+    k.lo = lo;
+    k.hi = hi;
     if (k.g1 - k.g0 > max_grants) max_grants = k.g1 - k.g0;
     ch.push_back(k);
     if (C == 0) break;
     c0 = c1;
   }
   const size_t nchunks = ch.size();
-  // --- input layout: per chunk, 11 segments (same order as mochi_batch) ---
   auto seg_bytes = [&](const Chunk& k, int i) -> size_t {
-    const size_t ng = k.g1 - k.g0, nc = k.c1 - k.c0, no = k.o1 - k.o0;
+    const size_t ng = k.g1 - k.g0, nc = k.c1 - k.c0, no = k.o1 - k.o0, nm = k.m1 - k.m0;
     switch (i) {
-      case 0: return (size_t)(k.hi - k.lo);
-      case 1: return sizeof(uint64_t) * ng;
-      case 2: return sizeof(uint32_t) * ng;
-      case 3: return (size_t)MOCHI_RSA_BYTES * ng;
-      case 4: return sizeof(uint16_t) * ng;
-      case 5: return ng;
-      case 6: case 7: return sizeof(uint32_t) * (nc + 1);
-      case 8: case 9: return no;
-      default: return (size_t)MOCHI_TXN_HASH_BYTES * nc;
+      case kBlob: return (size_t)(k.hi - k.lo);
+      case kGrantOff: return sizeof(uint64_t) * ng;
+      case kGrantLen: return sizeof(uint32_t) * ng;
+      case kSig: return (size_t)MOCHI_RSA_BYTES * ng;
+      case kSigner: return sizeof(uint16_t) * ng;
+      case kGrantKey: return ng;
+      case kCertGrantOff: case kCertOpOff: return sizeof(uint32_t) * (nc + 1);
+      case kOpKey: case kOpFlags: return no;
+      case kExpHash: return (size_t)MOCHI_TXN_HASH_BYTES * nc;
+      case kCertMgOff: return mg ? sizeof(uint32_t) * (nc + 1) : 0;
+      case kMgGrantOff: return mg ? sizeof(uint32_t) * (nm + 1) : 0;
+      case kOpObjTs: return b->op_object_ts ? sizeof(int64_t) * no : 0;
+      case kOpKeyOff: return b->op_key_off ? sizeof(uint64_t) * no : 0;
+      default: return b->op_key_len ? sizeof(uint32_t) * no : 0;
     }
   };
   auto seg_src = [&](const Chunk& k, int i) -> const void* {
     switch (i) {
-      case 0: return b->grant_bytes + k.lo;
-      case 1: return b->grant_off + k.g0;
-      case 2: return b->grant_len + k.g0;
-      case 3: return b->sig + (size_t)MOCHI_RSA_BYTES * k.g0;
-      case 4: return b->signer + k.g0;
-      case 5: return b->grant_key + k.g0;
-      case 6: case 7: return nullptr;  // rebased CSR, always staged
-      case 8: return b->op_key + k.o0;
-      case 9: return b->op_flags + k.o0;
-      default: return b->expected_hash + (size_t)MOCHI_TXN_HASH_BYTES * k.c0;
+      case kBlob: return b->grant_bytes + k.lo;
+      case kGrantOff: return b->grant_off + k.g0;
+      case kGrantLen: return b->grant_len + k.g0;
+      case kSig: return b->sig + (size_t)MOCHI_RSA_BYTES * k.g0;
+      case kSigner: return b->signer + k.g0;
+      case kGrantKey: return b->grant_key + k.g0;
+      case kOpKey: return b->op_key + k.o0;
+      case kOpFlags: return b->op_flags + k.o0;
+      case kExpHash: return b->expected_hash + (size_t)MOCHI_TXN_HASH_BYTES * k.c0;
+      case kOpObjTs: return b->op_object_ts ? b->op_object_ts + k.o0 : nullptr;
+      case kOpKeyOff: return b->op_key_off ? b->op_key_off + k.o0 : nullptr;
+      case kOpKeyLen: return b->op_key_len ? b->op_key_len + k.o0 : nullptr;
+      default: return nullptr;  // rebased CSR, always staged
     }
   };
+  auto rebased = [](int i) { return i == kCertGrantOff || i == kCertOpOff || i == kCertMgOff || i == kMgGrantOff; };
   size_t in_total = 0;
   for (auto& k : ch)
-    for (int i = 0; i < 11; i++) {
+    for (int i = 0; i < kNumSeg; i++) {
       k.seg[i] = in_total;
       in_total = align_up(in_total + seg_bytes(k, i), 256);
     }
@@ -519,7 +600,8 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
   };
   const size_t o_flags = take(N), o_ts = take(o->grant_ts ? sizeof(int64_t) * N : 0), o_acc = take(nbits_c),
                o_reason = take(o->cert_reason ? C : 0), o_fail = take(o->cert_fail_op ? C : 0),
-               o_gbits = take(o->grant_valid_bits ? nbits_g : 0);
+               o_gbits = take(o->grant_valid_bits ? nbits_g : 0), o_dec = take(o->op_decision ? O : 0),
+               o_g0 = take(o->op_g0 ? sizeof(uint32_t) * O : 0), o_ots = take(o->op_ts ? sizeof(int64_t) * O : 0);
   int rc;
   if ((rc = c->pin_in.ensure(in_total)) || (rc = c->dev_in.ensure(in_total)) || (rc = c->pin_out.ensure(out_total)) ||
       (rc = c->dev_out.ensure(out_total)) || (rc = ensure_scratch(c, max_grants)))
@@ -529,8 +611,8 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
     HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->chunk_ev.push_back(e);
   }
-  bool pinned[11];
-  for (int i = 0; i < 11; i++) pinned[i] = i != 6 && i != 7 && is_pinned(seg_src(ch[0], i));
+  bool pinned[kNumSeg];
+  for (int i = 0; i < kNumSeg; i++) pinned[i] = !rebased(i) && is_pinned(seg_src(ch[0], i));
   uint8_t* pin = (uint8_t*)c->pin_in.p;
   uint8_t* din = c->dev_in.as<uint8_t>();
   uint8_t* dout = c->dev_out.as<uint8_t>();
@@ -540,41 +622,54 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
   for (size_t j = 0; j < nchunks; j++) {
     Chunk& k = ch[j];
     // stage + upload
-    uint32_t* cg = (uint32_t*)(pin + k.seg[6]);
-    uint32_t* co = (uint32_t*)(pin + k.seg[7]);
+    uint32_t* cg = (uint32_t*)(pin + k.seg[kCertGrantOff]);
+    uint32_t* co = (uint32_t*)(pin + k.seg[kCertOpOff]);
     for (uint32_t x = k.c0; x <= k.c1; x++) {
       cg[x - k.c0] = b->cert_grant_off[x] - k.g0;
       co[x - k.c0] = b->cert_op_off[x] - k.o0;
     }
-    for (int i = 0; i < 11; i++) {
+    if (mg) {
+      uint32_t* cm = (uint32_t*)(pin + k.seg[kCertMgOff]);
+      uint32_t* mo = (uint32_t*)(pin + k.seg[kMgGrantOff]);
+      for (uint32_t x = k.c0; x <= k.c1; x++) cm[x - k.c0] = b->cert_mg_off[x] - k.m0;
+      for (uint32_t x = k.m0; x <= k.m1; x++) mo[x - k.m0] = b->mg_grant_off[x] - k.g0;
+    }
+    for (int i = 0; i < kNumSeg; i++) {
       const size_t n = seg_bytes(k, i);
       if (!n) continue;
       const void* src = pin + k.seg[i];
       if (pinned[i]) src = seg_src(k, i);
-      else if (i != 6 && i != 7) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
+      else if (!rebased(i)) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
       HIP_TRY(hipMemcpyAsync(din + k.seg[i], src, n, hipMemcpyHostToDevice, c->s_in));
     }
     HIP_TRY(hipEventRecord(c->chunk_ev[2 * j], c->s_in));
     // compute
     HIP_TRY(hipStreamWaitEvent(st, c->chunk_ev[2 * j], 0));
     if (j == 0) HIP_TRY(hipEventRecord(c->ev[1], st));
+    auto at = [&](int i) -> const void* { return seg_bytes(k, i) ? (const void*)(din + k.seg[i]) : nullptr; };
     mochi_batch db;
     memset(&db, 0, sizeof db);
     db.n_grants = k.g1 - k.g0;
     db.n_certs = k.c1 - k.c0;
     db.n_ops = k.o1 - k.o0;
-    db.grant_bytes_len = k.hi - k.lo;
-    db.grant_bytes = din + k.seg[0] - k.lo;  // kernels add the absolute grant_off
-    db.grant_off = (const uint64_t*)(din + k.seg[1]);
-    db.grant_len = (const uint32_t*)(din + k.seg[2]);
-    db.sig = din + k.seg[3];
-    db.signer = (const uint16_t*)(din + k.seg[4]);
-    db.grant_key = din + k.seg[5];
-    db.cert_grant_off = (const uint32_t*)(din + k.seg[6]);
-    db.cert_op_off = (const uint32_t*)(din + k.seg[7]);
-    db.op_key = din + k.seg[8];
-    db.op_flags = din + k.seg[9];
-    db.expected_hash = din + k.seg[10];
+    db.n_mgs = k.m1 - k.m0;
+    db.grant_bytes_len = k.hi;
+    db.grant_bytes = din + k.seg[kBlob] - k.lo;  // kernels add the absolute grant_off / op_key_off
+    db.grant_off = (const uint64_t*)(din + k.seg[kGrantOff]);
+    db.grant_len = (const uint32_t*)(din + k.seg[kGrantLen]);
+    db.sig = din + k.seg[kSig];
+    db.signer = (const uint16_t*)(din + k.seg[kSigner]);
+    db.grant_key = din + k.seg[kGrantKey];
+    db.cert_grant_off = (const uint32_t*)(din + k.seg[kCertGrantOff]);
+    db.cert_op_off = (const uint32_t*)(din + k.seg[kCertOpOff]);
+    db.op_key = din + k.seg[kOpKey];
+    db.op_flags = din + k.seg[kOpFlags];
+    db.expected_hash = din + k.seg[kExpHash];
+    db.cert_mg_off = (const uint32_t*)at(kCertMgOff);
+    db.mg_grant_off = (const uint32_t*)at(kMgGrantOff);
+    db.op_object_ts = (const int64_t*)at(kOpObjTs);
+    db.op_key_off = (const uint64_t*)at(kOpKeyOff);
+    db.op_key_len = (const uint32_t*)at(kOpKeyLen);
     mochi_verdicts dv;
     memset(&dv, 0, sizeof dv);
     dv.grant_flags = dout + o_flags + k.g0;
@@ -582,6 +677,9 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
     dv.cert_accept_bits = (uint32_t*)(dout + o_acc) + k.c0 / 32;
     dv.cert_reason = o->cert_reason ? dout + o_reason + k.c0 : nullptr;
     dv.cert_fail_op = o->cert_fail_op ? dout + o_fail + k.c0 : nullptr;
+    dv.op_decision = o->op_decision ? dout + o_dec + k.o0 : nullptr;
+    dv.op_g0 = o->op_g0 ? (uint32_t*)(dout + o_g0) + k.o0 : nullptr;
+    dv.op_ts = o->op_ts ? (int64_t*)(dout + o_ots) + k.o0 : nullptr;
     if ((rc = run_device(c, &db, p, &dv, st))) return rc;
     if (j + 1 == nchunks && o->grant_valid_bits && N)
       HIP_TRY(mochi::launch_pack_bits(dout + o_flags, N, MOCHI_GRANT_SIG_OK, (uint32_t*)(dout + o_gbits), st));
@@ -592,13 +690,16 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
     auto down = [&](size_t off, size_t bytes) -> hipError_t {
       return bytes ? hipMemcpyAsync(pout + off, dout + off, bytes, hipMemcpyDeviceToHost, c->s_out) : hipSuccess;
     };
-    const size_t ng = k.g1 - k.g0, nc = k.c1 - k.c0;
+    const size_t ng = k.g1 - k.g0, nc = k.c1 - k.c0, no = k.o1 - k.o0;
     const size_t acc_words = j + 1 == nchunks ? nbits_c / 4 - k.c0 / 32 : nc / 32;
     if (o->grant_flags) HIP_TRY(down(o_flags + k.g0, ng));
     if (o->grant_ts) HIP_TRY(down(o_ts + sizeof(int64_t) * k.g0, sizeof(int64_t) * ng));
     HIP_TRY(down(o_acc + 4 * (size_t)(k.c0 / 32), 4 * acc_words));
     if (o->cert_reason) HIP_TRY(down(o_reason + k.c0, nc));
     if (o->cert_fail_op) HIP_TRY(down(o_fail + k.c0, nc));
+    if (o->op_decision) HIP_TRY(down(o_dec + k.o0, no));
+    if (o->op_g0) HIP_TRY(down(o_g0 + sizeof(uint32_t) * k.o0, sizeof(uint32_t) * no));
+    if (o->op_ts) HIP_TRY(down(o_ots + sizeof(int64_t) * k.o0, sizeof(int64_t) * no));
     if (j + 1 == nchunks && o->grant_valid_bits) HIP_TRY(down(o_gbits, nbits_g));
   }
   HIP_TRY(hipEventRecord(c->ev[3], c->s_out));
@@ -609,10 +710,11 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
   (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);  // last download (not overlapped)
   (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
   void* dsts[] = {o->grant_flags, o->grant_ts, o->cert_accept_bits, o->cert_reason, o->cert_fail_op,
-                  o->grant_valid_bits};
-  const size_t offs[] = {o_flags, o_ts, o_acc, o_reason, o_fail, o_gbits};
-  const size_t lens[] = {(size_t)N, sizeof(int64_t) * N, nbits_c, (size_t)C, (size_t)C, nbits_g};
-  for (int i = 0; i < 6; i++)
+                  o->grant_valid_bits, o->op_decision, o->op_g0, o->op_ts};
+  const size_t offs[] = {o_flags, o_ts, o_acc, o_reason, o_fail, o_gbits, o_dec, o_g0, o_ots};
+  const size_t lens[] = {(size_t)N, sizeof(int64_t) * N, nbits_c, (size_t)C, (size_t)C, nbits_g,
+                         (size_t)O, sizeof(uint32_t) * O, sizeof(int64_t) * O};
+  for (int i = 0; i < 9; i++)
     if (dsts[i] && lens[i]) memcpy(dsts[i], pout + offs[i], lens[i]);
   return MOCHI_OK;
 }
@@ -620,48 +722,77 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
 // ---- Write2ToServer wire path -------------------------------------------------
 // Decode on the device (w2_decode.hip), then the ordinary verify path over the
 // decoded batch, then the per-message status fix-up.  All pointers device.
-int run_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
-                      uint8_t* status, hipStream_t st, mochi::W2Args* decoded_only = nullptr) {
+// Decode, phase 1 (w2_decode.hip): validate + count + CSR scans for the M
+// messages of `w`.  cnt: 6*(M+1) device words (counts and CSR offsets of this
+// batch, so a pipelined caller can count chunk j+1 while chunk j verifies);
+// the totals (N, O, n_mgs) land in tot_host (pinned) once ev_tot completes.
+int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_t* cnt, uint32_t* tot_host,
+             hipEvent_t ev_tot, hipStream_t st, mochi::W2Args* a) {
   const uint32_t M = w->n_msgs;
-  if (c->n_ids != c->n_keys) return fail(MOCHI_EINVAL, "server ids not set (mochi_ctx_set_server_ids)");
+  const size_t m1 = (size_t)M + 1;
   size_t scan_bytes = 0;
   HIP_TRY(mochi::w2_scan_temp_bytes(M + 1, &scan_bytes));
-  int rc;
-  if ((rc = c->w2_cnt_g.ensure(4 * ((size_t)M + 1))) || (rc = c->w2_cnt_o.ensure(4 * ((size_t)M + 1))) ||
-      (rc = c->w2_scan.ensure(scan_bytes)) || (rc = c->w2_cg.ensure(4 * ((size_t)M + 1))) ||
-      (rc = c->w2_co.ensure(4 * ((size_t)M + 1))) || (rc = c->w2_tot.ensure(8)) ||
-      (!status && (rc = c->w2_status.ensure(M ? M : 1))))
-    return rc;
-  mochi::W2Args a;
-  memset(&a, 0, sizeof a);
-  a.wire = w->wire;
-  a.msg_off = w->msg_off;
-  a.msg_len = w->msg_len;
-  a.M = M;
-  a.flags_off = w->op_flags_off;
-  a.flags_in = w->op_flags;
-  a.ids = c->ids.as<uint8_t>();
-  a.id_off = c->id_off.as<uint32_t>();
-  a.n_ids = c->n_ids;
-  a.cnt_g = c->w2_cnt_g.as<uint32_t>();
-  a.cnt_o = c->w2_cnt_o.as<uint32_t>();
-  a.status = status ? status : c->w2_status.as<uint8_t>();
-  a.scan_temp = c->w2_scan.p;
-  a.scan_temp_bytes = c->w2_scan.cap;
-  a.cert_grant_off = c->w2_cg.as<uint32_t>();
-  a.cert_op_off = c->w2_co.as<uint32_t>();
-  HIP_TRY(mochi::launch_w2_count(a, st));
-  // totals decide the decoded-array sizes
-  uint32_t* tot = (uint32_t*)c->w2_tot.p;
-  HIP_TRY(hipMemcpyAsync(tot, a.cert_grant_off + M, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(tot + 1, a.cert_op_off + M, 4, hipMemcpyDeviceToHost, st));
+  if (scan_bytes > c->w2_scan.cap) {
+    HIP_TRY(hipStreamSynchronize(st));  // the scan scratch may be in use by an earlier chunk
+    int rc = c->w2_scan.ensure(scan_bytes);
+    if (rc) return rc;
+  }
+  memset(a, 0, sizeof *a);
+  a->wire = w->wire;
+  a->msg_off = w->msg_off;
+  a->msg_len = w->msg_len;
+  a->M = M;
+  a->flags_off = w->op_flags_off;
+  a->flags_in = w->op_flags;
+  a->ots_in = w->op_object_ts;
+  a->ids = c->ids.as<uint8_t>();
+  a->id_off = c->id_off.as<uint32_t>();
+  a->n_ids = c->n_ids;
+  a->cnt_g = cnt;
+  a->cnt_o = cnt + m1;
+  a->cnt_m = cnt + 2 * m1;
+  a->cert_grant_off = cnt + 3 * m1;
+  a->cert_op_off = cnt + 4 * m1;
+  a->cert_mg_off = cnt + 5 * m1;
+  a->status = status;
+  a->scan_temp = c->w2_scan.p;
+  a->scan_temp_bytes = c->w2_scan.cap;
+  HIP_TRY(mochi::launch_w2_count(*a, st));
+  HIP_TRY(hipMemcpyAsync(tot_host, a->cert_grant_off + M, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(tot_host + 1, a->cert_op_off + M, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(tot_host + 2, a->cert_mg_off + M, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(ev_tot, st));
+  return MOCHI_OK;
+}
+
+// Grow a decode buffer; if it must be reallocated, first let the stream drain
+// (an earlier chunk's kernels may still read the old allocation).
+int grow(DevBuf& b, size_t bytes, hipStream_t st) {
+  if (bytes <= b.cap) return MOCHI_OK;
   HIP_TRY(hipStreamSynchronize(st));
-  const uint32_t N = tot[0], O = tot[1];
-  if ((rc = c->w2_goff.ensure(8 * (size_t)N)) || (rc = c->w2_glen.ensure(4 * (size_t)N)) ||
-      (rc = c->w2_sig.ensure((size_t)MOCHI_RSA_BYTES * N)) || (rc = c->w2_signer.ensure(2 * (size_t)N)) ||
-      (rc = c->w2_gkey.ensure(N)) || (rc = c->w2_okey.ensure(O)) || (rc = c->w2_oflags.ensure(O)) ||
-      (rc = c->w2_sigsrc.ensure(8 * (size_t)N)))
+  return b.ensure(bytes);
+}
+
+// Decode, phase 2: emit the SoA batch (N grants, O ops, NM MultiGrants from
+// phase 1), then the verify path and the per-message status fix-up.  Per-op
+// outputs follow the caller's op_flags_off layout (`op_out_off`, device).
+int w2_verify(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+              mochi::W2Args& a, uint32_t N, uint32_t O, uint32_t NM, const uint32_t* op_out_off, hipStream_t st,
+              bool decode_only) {
+  int rc;
+  if ((rc = grow(c->w2_goff, 8 * (size_t)N, st)) || (rc = grow(c->w2_glen, 4 * (size_t)N, st)) ||
+      (rc = grow(c->w2_sig, (size_t)MOCHI_RSA_BYTES * N, st)) || (rc = grow(c->w2_signer, 2 * (size_t)N, st)) ||
+      (rc = grow(c->w2_gkey, N, st)) || (rc = grow(c->w2_okey, O, st)) || (rc = grow(c->w2_oflags, O, st)) ||
+      (rc = grow(c->w2_sigsrc, 8 * (size_t)N, st)) || (rc = grow(c->w2_mgo, 4 * ((size_t)NM + 1), st)) ||
+      (rc = grow(c->w2_ots, 8 * (size_t)O, st)) || (rc = grow(c->w2_okoff, 8 * (size_t)O, st)) ||
+      (rc = grow(c->w2_oklen, 4 * (size_t)O, st)))
     return rc;
+  if (!decode_only) {  // the verify scratch grows only once the stream has drained
+    const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
+    if (sizeof(uint32_t) * mochi::kL * slots > c->xbuf.cap || sizeof(uint32_t) * 8 * (size_t)N > c->digest.cap)
+      HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = ensure_scratch(c, N))) return rc;
+  }
   a.N = N;
   a.sig_src = c->w2_sigsrc.as<uint64_t>();
   a.grant_off = c->w2_goff.as<uint64_t>();
@@ -671,16 +802,18 @@ int run_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_par
   a.grant_key = c->w2_gkey.as<uint8_t>();
   a.op_key = c->w2_okey.as<uint8_t>();
   a.op_flags = c->w2_oflags.as<uint8_t>();
+  a.op_object_ts = c->w2_ots.as<int64_t>();
+  a.op_key_off = c->w2_okoff.as<uint64_t>();
+  a.op_key_len = c->w2_oklen.as<uint32_t>();
+  a.mg_grant_off = c->w2_mgo.as<uint32_t>();
   HIP_TRY(mochi::launch_w2_emit(a, st));
-  if (decoded_only) {
-    *decoded_only = a;
-    return MOCHI_OK;
-  }
+  if (decode_only) return MOCHI_OK;
   mochi_batch db;
   memset(&db, 0, sizeof db);
   db.n_grants = N;
-  db.n_certs = M;
+  db.n_certs = a.M;
   db.n_ops = O;
+  db.n_mgs = NM;
   db.grant_bytes_len = w->wire_len;
   db.grant_bytes = w->wire;
   db.grant_off = a.grant_off;
@@ -693,13 +826,42 @@ int run_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_par
   db.op_key = a.op_key;
   db.op_flags = a.op_flags;
   db.expected_hash = w->expected_hash;
+  db.cert_mg_off = a.cert_mg_off;
+  db.mg_grant_off = a.mg_grant_off;
+  db.op_object_ts = a.op_object_ts;
+  db.op_key_off = a.op_key_off;
+  db.op_key_len = a.op_key_len;
   mochi_verdicts dv;
   memset(&dv, 0, sizeof dv);
   dv.cert_accept_bits = o->cert_accept_bits;
   dv.cert_reason = o->cert_reason;
   dv.cert_fail_op = o->cert_fail_op;
-  if ((rc = run_device(c, &db, p, &dv, st))) return rc;
-  HIP_TRY(mochi::launch_w2_fixup(a, o->cert_accept_bits, o->cert_reason, o->cert_fail_op, st));
+  dv.op_decision = o->op_decision;
+  dv.op_g0 = o->op_g0;
+  dv.op_ts = o->op_ts;
+  if ((rc = run_device(c, &db, p, &dv, st, op_out_off))) return rc;
+  HIP_TRY(mochi::launch_w2_fixup(a, o->cert_accept_bits, o->cert_reason, o->cert_fail_op, o->op_decision, o->op_g0,
+                                 o->op_ts, st));
+  return MOCHI_OK;
+}
+
+// Device-resident wire batch, one shot (mochi_verify_write2_device).
+int run_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+                      uint8_t* status, hipStream_t st) {
+  const uint32_t M = w->n_msgs;
+  if (c->n_ids != c->n_keys) return fail(MOCHI_EINVAL, "server ids not set (mochi_ctx_set_server_ids)");
+  int rc;
+  if ((rc = c->w2_cnt.ensure(4 * 6 * ((size_t)M + 1))) || (rc = c->w2_tot.ensure(16)) ||
+      (!status && (rc = c->w2_status.ensure(M ? M : 1))))
+    return rc;
+  HIP_TRY(scratch_acquire(c, st));
+  mochi::W2Args a;
+  uint32_t* tot = (uint32_t*)c->w2_tot.p;
+  if ((rc = w2_count(c, w, status ? status : c->w2_status.as<uint8_t>(), c->w2_cnt.as<uint32_t>(), tot, c->ev_tot, st, &a)))
+    return rc;
+  HIP_TRY(hipEventSynchronize(c->ev_tot));
+  if ((rc = w2_verify(c, w, p, o, a, tot[0], tot[1], tot[2], w->op_flags_off, st, false))) return rc;
+  HIP_TRY(scratch_release(c, st));
   return MOCHI_OK;
 }
 
@@ -711,6 +873,11 @@ int check_write2_header(const mochi_ctx* c, const mochi_write2_batch* w, const m
   if (w->n_msgs && (!o->cert_accept_bits || !w->wire || !w->msg_off || !w->msg_len || !w->expected_hash))
     return fail(MOCHI_EINVAL, "wire / msg_off / msg_len / expected_hash / cert_accept_bits required");
   if (w->op_flags_off && !w->op_flags) return fail(MOCHI_EINVAL, "op_flags required with op_flags_off");
+  if ((o->op_decision || o->op_g0 || o->op_ts) && !w->op_flags_off)
+    return fail(MOCHI_EINVAL, "per-op outputs on the wire path need op_flags_off (their layout)");
+  if (w->op_object_ts && !w->op_flags_off) return fail(MOCHI_EINVAL, "op_object_ts needs op_flags_off");
+  if ((p->quorum_mode & ~(uint32_t)(MOCHI_Q_DISTINCT_SIGNERS | MOCHI_Q_BIND)) != 0)
+    return fail(MOCHI_EINVAL, "unknown quorum_mode bits 0x%x", p->quorum_mode);
   if (p->replication_factor == 0) return fail(MOCHI_EINVAL, "replication_factor must be > 0");
   return MOCHI_OK;
 }
@@ -819,7 +986,7 @@ int mochi_verify_write2(mochi_ctx* c, const mochi_write2_batch* w, const mochi_p
 int mochi_write2_decode(mochi_ctx* c, const mochi_write2_batch* w, mochi_write2_decoded* out) {
   if (!out) return fail(MOCHI_EINVAL, "null argument");
   memset(out, 0, sizeof *out);
-  mochi_params p = {1, 1, {0, 0}};
+  mochi_params p = {1, 1, 0, 0};
   mochi_verdicts o;
   memset(&o, 0, sizeof o);
   uint32_t dummy = 0;
@@ -841,9 +1008,22 @@ void mochi_write2_decoded_free(mochi_write2_decoded* d) {
   free(d->op_key);
   free(d->op_flags);
   free(d->msg_status);
+  free(d->cert_mg_off);
+  free(d->mg_grant_off);
+  free(d->op_key_off);
+  free(d->op_key_len);
   memset(d, 0, sizeof *d);
 }
 
+// ---- Write2 wire path, host memory: chunked pipeline -------------------------
+//
+// Messages are cut into chunks of whole messages (multiples of 32, so each
+// chunk's accept bits start on a word) of ~chunk_grants * 512 wire bytes.  For
+// chunk j: stage + upload (copy-in stream), then on the context stream the
+// decode count phase and its totals; chunk j-1's emit + verify + fix-up is
+// enqueued once ITS totals are on the host, so the host waits only for count
+// kernels while the device verifies the previous chunk and the copy engines
+// move the next one.  Verdicts come down per chunk on the copy-out stream.
 static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
                               uint8_t* msg_status, mochi_write2_decoded* dec) {
   int rc;
@@ -851,63 +1031,197 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   for (uint32_t m = 0; m < M; m++)
     if (w->msg_off[m] > w->wire_len || w->msg_len[m] > w->wire_len - w->msg_off[m])
       return fail(MOCHI_EINVAL, "message %u lies outside wire", m);
+  if (w->op_flags_off) {  // the device trusts these offsets: validate them here
+    if (w->op_flags_off[0] != 0) return fail(MOCHI_EINVAL, "op_flags_off[0] must be 0");
+    for (uint32_t m = 0; m < M; m++)
+      if (w->op_flags_off[m + 1] < w->op_flags_off[m]) return fail(MOCHI_EINVAL, "op_flags_off decreases at %u", m);
+  }
+  if (c->n_ids != c->n_keys) return fail(MOCHI_EINVAL, "server ids not set (mochi_ctx_set_server_ids)");
   std::lock_guard<std::mutex> lk(c->mu);
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
-  const size_t O_in = w->op_flags_off ? w->op_flags_off[M] : 0;
-  struct Seg {
-    const void* src;
-    size_t bytes, off;
-  } in[] = {{w->wire, (size_t)w->wire_len, 0},
-            {w->msg_off, 8 * (size_t)M, 0},
-            {w->msg_len, 4 * (size_t)M, 0},
-            {w->op_flags_off, w->op_flags_off ? 4 * ((size_t)M + 1) : 0, 0},
-            {w->op_flags, O_in, 0},
-            {w->expected_hash, (size_t)MOCHI_TXN_HASH_BYTES * M, 0}};
-  size_t in_total = 0;
-  for (auto& sg : in) {
-    sg.off = in_total;
-    in_total = align_up(in_total + sg.bytes, 256);
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{save};
+  const uint32_t* ofo = w->op_flags_off;
+  const size_t O_in = ofo ? ofo[M] : 0;
+  // --- chunks ---
+  struct Chunk {
+    uint32_t m0, m1;
+    uint64_t lo, hi;  // wire byte range
+    size_t seg[7], cnt;
+  };
+  std::vector<Chunk> ch;
+  const uint64_t target = dec ? UINT64_MAX : (uint64_t)c->chunk_grants * 512;
+  for (uint32_t m0 = 0; m0 < M || ch.empty();) {
+    uint32_t m1 = m0;
+    uint64_t bytes = 0;
+    do {
+      const uint32_t next = m1 + 32 < M ? m1 + 32 : M;
+      for (uint32_t m = m1; m < next; m++) bytes += w->msg_len[m];
+      m1 = next;
+    } while (m1 < M && bytes < target);
+    Chunk k{};
+    k.m0 = m0;
+    k.m1 = m1;
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t m = m0; m < m1; m++) {
+      lo = w->msg_off[m] < lo ? w->msg_off[m] : lo;
+      hi = w->msg_off[m] + w->msg_len[m] > hi ? w->msg_off[m] + w->msg_len[m] : hi;
+    }
+    if (lo == UINT64_MAX) lo = hi = 0;
+    k.lo = lo;
+    k.hi = hi;
+    ch.push_back(k);
+    if (M == 0) break;
+    m0 = m1;
+  }
+  const size_t nch = ch.size();
+  // --- input segments: wire slice, msg_off, msg_len, op_flags_off (rebased), op_flags, op_object_ts, hash ---
+  auto seg_bytes = [&](const Chunk& k, int i) -> size_t {
+    const size_t nm = k.m1 - k.m0, no = ofo ? ofo[k.m1] - ofo[k.m0] : 0;
+    switch (i) {
+      case 0: return (size_t)(k.hi - k.lo);
+      case 1: return 8 * nm;
+      case 2: return 4 * nm;
+      case 3: return ofo ? 4 * (nm + 1) : 0;
+      case 4: return ofo ? no : 0;
+      case 5: return ofo && w->op_object_ts ? 8 * no : 0;
+      default: return (size_t)MOCHI_TXN_HASH_BYTES * nm;
+    }
+  };
+  auto seg_src = [&](const Chunk& k, int i) -> const void* {
+    switch (i) {
+      case 0: return w->wire + k.lo;
+      case 1: return w->msg_off + k.m0;
+      case 2: return w->msg_len + k.m0;
+      case 3: return nullptr;  // rebased, staged
+      case 4: return ofo ? w->op_flags + ofo[k.m0] : nullptr;
+      case 5: return ofo && w->op_object_ts ? w->op_object_ts + ofo[k.m0] : nullptr;
+      default: return w->expected_hash + (size_t)MOCHI_TXN_HASH_BYTES * k.m0;
+    }
+  };
+  size_t in_total = 0, cnt_total = 0;
+  for (auto& k : ch) {
+    for (int i = 0; i < 7; i++) {
+      k.seg[i] = in_total;
+      in_total = align_up(in_total + seg_bytes(k, i), 256);
+    }
+    k.cnt = cnt_total;
+    cnt_total += 6 * ((size_t)(k.m1 - k.m0) + 1);
   }
   const size_t nbits = ((size_t)M + 31) / 32 * 4;
-  const size_t o_acc = 0, o_reason = align_up(nbits, 256), o_fail = o_reason + align_up(M, 256),
-               o_status = o_fail + align_up(M, 256), out_total = o_status + align_up(M ? M : 1, 256);
-  hipStream_t st = c->stream;
+  size_t out_total = 0;
+  auto take = [&](size_t bytes) {
+    const size_t off = out_total;
+    out_total = align_up(out_total + bytes, 256);
+    return off;
+  };
+  const size_t o_acc = take(nbits), o_reason = take(M), o_fail = take(M), o_status = take(M ? M : 1),
+               o_dec = take(o->op_decision ? O_in : 0), o_g0 = take(o->op_g0 ? 4 * O_in : 0),
+               o_ots = take(o->op_ts ? 8 * O_in : 0);
   if ((rc = c->pin_in.ensure(in_total)) || (rc = c->dev_in.ensure(in_total)) || (rc = c->pin_out.ensure(out_total)) ||
-      (rc = c->dev_out.ensure(out_total))) {
-    (void)hipSetDevice(save);
+      (rc = c->dev_out.ensure(out_total)) || (rc = c->w2_cnt.ensure(4 * cnt_total)) ||
+      (rc = c->w2_tot.ensure(16 * nch)))
     return rc;
+  while (c->chunk_ev.size() < 2 * nch) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->chunk_ev.push_back(e);
+  }
+  while (c->tot_ev.size() < nch) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->tot_ev.push_back(e);
   }
   uint8_t* pin = (uint8_t*)c->pin_in.p;
   uint8_t* din = c->dev_in.as<uint8_t>();
   uint8_t* dout = c->dev_out.as<uint8_t>();
-  for (auto& sg : in)
-    if (sg.bytes) par_memcpy(pin + sg.off, sg.src, sg.bytes);
-  rc = MOCHI_OK;
-  if (hipEventRecord(c->ev[0], st) != hipSuccess ||
-      hipMemcpyAsync(din, pin, in_total, hipMemcpyHostToDevice, st) != hipSuccess)
-    rc = fail(MOCHI_EHIP, "H2D copy failed");
-  mochi_write2_batch dw = *w;
-  dw.wire = din + in[0].off;
-  dw.msg_off = (const uint64_t*)(din + in[1].off);
-  dw.msg_len = (const uint32_t*)(din + in[2].off);
-  dw.op_flags_off = w->op_flags_off ? (const uint32_t*)(din + in[3].off) : nullptr;
-  dw.op_flags = w->op_flags_off ? din + in[4].off : nullptr;
-  dw.expected_hash = din + in[5].off;
-  mochi_verdicts dv;
-  memset(&dv, 0, sizeof dv);
-  dv.cert_accept_bits = (uint32_t*)(dout + o_acc);
-  dv.cert_reason = dout + o_reason;
-  dv.cert_fail_op = dout + o_fail;
-  mochi::W2Args da;
-  if (!rc) rc = run_write2_device(c, &dw, p, &dv, dout + o_status, st, dec ? &da : nullptr);
-  if (!rc && dec) {
-    // decode-only: copy the decoded SoA back (tests / inspection)
-    const uint32_t N = ((uint32_t*)c->w2_tot.p)[0], O = ((uint32_t*)c->w2_tot.p)[1];
+  uint8_t* pout = (uint8_t*)c->pin_out.p;
+  uint32_t* tot = (uint32_t*)c->w2_tot.p;
+  hipStream_t st = c->stream;
+  std::vector<mochi_write2_batch> dws(nch);
+  std::vector<mochi::W2Args> args(nch);
+  HIP_TRY(scratch_acquire(c, st));
+  HIP_TRY(hipEventRecord(c->ev[0], c->s_in));
+  // phase 2 + download of chunk j (its totals must be on the host)
+  auto finish = [&](size_t j) -> int {
+    Chunk& k = ch[j];
+    HIP_TRY(hipEventSynchronize(c->tot_ev[j]));
+    const uint32_t* t = tot + 4 * j;
+    const uint32_t nm = k.m1 - k.m0, o0 = ofo ? ofo[k.m0] : 0;
+    mochi_verdicts dv;
+    memset(&dv, 0, sizeof dv);
+    dv.cert_accept_bits = (uint32_t*)(dout + o_acc) + k.m0 / 32;
+    dv.cert_reason = dout + o_reason + k.m0;
+    dv.cert_fail_op = dout + o_fail + k.m0;
+    dv.op_decision = o->op_decision ? dout + o_dec + o0 : nullptr;
+    dv.op_g0 = o->op_g0 ? (uint32_t*)(dout + o_g0) + o0 : nullptr;
+    dv.op_ts = o->op_ts ? (int64_t*)(dout + o_ots) + o0 : nullptr;
+    int r = w2_verify(c, &dws[j], p, &dv, args[j], t[0], t[1], t[2], dws[j].op_flags_off, st, dec != nullptr);
+    if (r) return r;
+    if (dec) return MOCHI_OK;
+    if (j + 1 == nch) HIP_TRY(hipEventRecord(c->ev[2], st));
+    HIP_TRY(hipEventRecord(c->chunk_ev[2 * j + 1], st));
+    HIP_TRY(hipStreamWaitEvent(c->s_out, c->chunk_ev[2 * j + 1], 0));
+    auto down = [&](size_t off, size_t bytes) -> hipError_t {
+      return bytes ? hipMemcpyAsync(pout + off, dout + off, bytes, hipMemcpyDeviceToHost, c->s_out) : hipSuccess;
+    };
+    const size_t no = ofo ? ofo[k.m1] - o0 : 0;
+    const size_t acc_words = j + 1 == nch ? nbits / 4 - k.m0 / 32 : nm / 32;
+    HIP_TRY(down(o_acc + 4 * (size_t)(k.m0 / 32), 4 * acc_words));
+    HIP_TRY(down(o_reason + k.m0, nm));
+    HIP_TRY(down(o_fail + k.m0, nm));
+    HIP_TRY(down(o_status + k.m0, nm));
+    if (o->op_decision) HIP_TRY(down(o_dec + o0, no));
+    if (o->op_g0) HIP_TRY(down(o_g0 + 4 * (size_t)o0, 4 * no));
+    if (o->op_ts) HIP_TRY(down(o_ots + 8 * (size_t)o0, 8 * no));
+    return MOCHI_OK;
+  };
+  for (size_t j = 0; j < nch; j++) {
+    Chunk& k = ch[j];
+    const uint32_t nm = k.m1 - k.m0;
+    if (ofo) {
+      uint32_t* f = (uint32_t*)(pin + k.seg[3]);
+      for (uint32_t m = k.m0; m <= k.m1; m++) f[m - k.m0] = ofo[m] - ofo[k.m0];
+    }
+    for (int i = 0; i < 7; i++) {
+      const size_t n = seg_bytes(k, i);
+      if (!n) continue;
+      if (i != 3) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
+      HIP_TRY(hipMemcpyAsync(din + k.seg[i], pin + k.seg[i], n, hipMemcpyHostToDevice, c->s_in));
+    }
+    HIP_TRY(hipEventRecord(c->chunk_ev[2 * j], c->s_in));
+    mochi_write2_batch& dw = dws[j];
+    memset(&dw, 0, sizeof dw);
+    dw.n_msgs = nm;
+    dw.wire_len = k.hi;
+    dw.wire = din + k.seg[0] - k.lo;  // message offsets stay absolute
+    dw.msg_off = (const uint64_t*)(din + k.seg[1]);
+    dw.msg_len = (const uint32_t*)(din + k.seg[2]);
+    dw.op_flags_off = ofo ? (const uint32_t*)(din + k.seg[3]) : nullptr;
+    dw.op_flags = ofo ? din + k.seg[4] : nullptr;
+    dw.op_object_ts = seg_bytes(k, 5) ? (const int64_t*)(din + k.seg[5]) : nullptr;
+    dw.expected_hash = din + k.seg[6];
+    HIP_TRY(hipStreamWaitEvent(st, c->chunk_ev[2 * j], 0));
+    if (j == 0) HIP_TRY(hipEventRecord(c->ev[1], st));
+    if ((rc = w2_count(c, &dw, dout + o_status + k.m0, c->w2_cnt.as<uint32_t>() + k.cnt, tot + 4 * j, c->tot_ev[j], st,
+                       &args[j])))
+      return rc;
+    if (j > 0 && (rc = finish(j - 1))) return rc;
+  }
+  if ((rc = finish(nch - 1))) return rc;
+  HIP_TRY(scratch_release(c, st));
+  if (dec) {
+    // decode-only (one chunk): copy the decoded SoA back (tests / inspection)
+    const mochi::W2Args& da = args[0];
+    const uint32_t N = tot[0], O = tot[1], NM = tot[2];
     dec->n_msgs = M;
     dec->n_grants = N;
     dec->n_ops = O;
+    dec->n_mgs = NM;
     dec->grant_off = (uint64_t*)malloc(8 * (size_t)N + 8);
     dec->grant_len = (uint32_t*)malloc(4 * (size_t)N + 4);
     dec->sig = (uint8_t*)malloc((size_t)MOCHI_RSA_BYTES * N + 1);
@@ -918,6 +1232,10 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     dec->op_key = (uint8_t*)malloc((size_t)O + 1);
     dec->op_flags = (uint8_t*)malloc((size_t)O + 1);
     dec->msg_status = (uint8_t*)malloc((size_t)M + 1);
+    dec->cert_mg_off = (uint32_t*)malloc(4 * ((size_t)M + 1));
+    dec->mg_grant_off = (uint32_t*)malloc(4 * ((size_t)NM + 1));
+    dec->op_key_off = (uint64_t*)malloc(8 * (size_t)O + 8);
+    dec->op_key_len = (uint32_t*)malloc(4 * (size_t)O + 4);
     struct {
       void* dst;
       const void* src;
@@ -926,27 +1244,28 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
               {dec->sig, da.sig, (size_t)MOCHI_RSA_BYTES * N},   {dec->signer, da.signer, 2 * (size_t)N},
               {dec->grant_key, da.grant_key, N},                 {dec->cert_grant_off, da.cert_grant_off, 4 * ((size_t)M + 1)},
               {dec->cert_op_off, da.cert_op_off, 4 * ((size_t)M + 1)}, {dec->op_key, da.op_key, O},
-              {dec->op_flags, da.op_flags, O},                   {dec->msg_status, da.status, M}};
+              {dec->op_flags, da.op_flags, O},                   {dec->msg_status, da.status, M},
+              {dec->cert_mg_off, da.cert_mg_off, 4 * ((size_t)M + 1)}, {dec->mg_grant_off, da.mg_grant_off, 4 * ((size_t)NM + 1)},
+              {dec->op_key_off, da.op_key_off, 8 * (size_t)O},   {dec->op_key_len, da.op_key_len, 4 * (size_t)O}};
     for (auto& x : cp)
-      if (!rc && x.n && hipMemcpyAsync(x.dst, x.src, x.n, hipMemcpyDeviceToHost, st) != hipSuccess)
-        rc = fail(MOCHI_EHIP, "decode copy-back failed");
-    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = fail(MOCHI_EHIP, "decode sync failed");
-    (void)hipSetDevice(save);
-    return rc;
+      if (x.n) HIP_TRY(hipMemcpyAsync(x.dst, x.src, x.n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return MOCHI_OK;
   }
-  if (!rc && (hipMemcpyAsync(c->pin_out.p, dout, out_total, hipMemcpyDeviceToHost, st) != hipSuccess ||
-              hipEventRecord(c->ev[3], st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess))
-    rc = fail(MOCHI_EHIP, "write2 path failed: %s", hipGetErrorString(hipGetLastError()));
-  if (!rc) {
-    (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
-    const uint8_t* po = (const uint8_t*)c->pin_out.p;
-    memcpy(o->cert_accept_bits, po + o_acc, nbits);
-    if (o->cert_reason) memcpy(o->cert_reason, po + o_reason, M);
-    if (o->cert_fail_op) memcpy(o->cert_fail_op, po + o_fail, M);
-    if (msg_status) memcpy(msg_status, po + o_status, M);
-  }
-  (void)hipSetDevice(save);
-  return rc;
+  HIP_TRY(hipEventRecord(c->ev[3], c->s_out));
+  HIP_TRY(hipStreamSynchronize(c->s_out));
+  (void)hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[1]);
+  (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);
+  (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
+  memcpy(o->cert_accept_bits, pout + o_acc, nbits);
+  if (o->cert_reason) memcpy(o->cert_reason, pout + o_reason, M);
+  if (o->cert_fail_op) memcpy(o->cert_fail_op, pout + o_fail, M);
+  if (msg_status) memcpy(msg_status, pout + o_status, M);
+  if (o->op_decision) memcpy(o->op_decision, pout + o_dec, O_in);
+  if (o->op_g0) memcpy(o->op_g0, pout + o_g0, 4 * O_in);
+  if (o->op_ts) memcpy(o->op_ts, pout + o_ots, 8 * O_in);
+  return MOCHI_OK;
 }
 
 int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const uint16_t* signer, uint8_t* out_be,

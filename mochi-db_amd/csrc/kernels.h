@@ -22,7 +22,12 @@ struct LaunchArgs {
   const uint8_t* op_key;
   const uint8_t* op_flags;
   const uint8_t* expected_hash;
-  uint32_t majority, strict_gt;
+  const uint32_t* cert_mg_off;   // [C+1] or null (MultiGrant = signer run)
+  const uint32_t* mg_grant_off;  // [n_mgs+1] or null
+  const int64_t* op_object_ts;   // [O] or null
+  const uint64_t* op_key_off;    // [O] or null (MOCHI_Q_BIND)
+  const uint32_t* op_key_len;    // [O] or null
+  uint32_t majority, strict_gt, quorum_mode;
   const KeyEntry* keys;
   // scratch (context-owned)
   uint32_t* digest;    // [8][N]
@@ -40,6 +45,10 @@ struct LaunchArgs {
   uint32_t* cert_accept_bits;
   uint8_t* cert_reason;   // may be null
   uint8_t* cert_fail_op;  // may be null
+  uint8_t* op_decision;   // [O] may be null
+  uint32_t* op_g0;        // [O] may be null
+  int64_t* op_ts;         // [O] may be null
+  const uint32_t* op_out_off;  // [C+1] per-op output positions; null = cert_op_off
   // mochi_rsa_public_op only: raw s^65537 mod n words [N][64] (else null)
   uint32_t* dbg_y;
   bool skip_prep_tally;
@@ -69,17 +78,20 @@ struct W2Args {
   uint32_t M;
   const uint32_t* flags_off;  // [M+1] or null
   const uint8_t* flags_in;
+  const int64_t* ots_in;      // aligned with flags_in, or null
   const uint8_t* ids;         // server-id table
   const uint32_t* id_off;
   uint32_t n_ids;
   // scratch / outputs
   uint32_t* cnt_g;  // [M+1]
   uint32_t* cnt_o;  // [M+1]
+  uint32_t* cnt_m;  // [M+1] MultiGrants
   uint8_t* status;  // [M]
   void* scan_temp;
   size_t scan_temp_bytes;
   uint32_t* cert_grant_off;  // [M+1]
   uint32_t* cert_op_off;     // [M+1]
+  uint32_t* cert_mg_off;     // [M+1]
   uint32_t N;          // decoded grant total (emit)
   uint64_t* sig_src;   // [N] wire offset of each signature (emit -> k_w2_sig)
   uint64_t* grant_off;
@@ -89,12 +101,16 @@ struct W2Args {
   uint8_t* grant_key;
   uint8_t* op_key;
   uint8_t* op_flags;
+  int64_t* op_object_ts;
+  uint64_t* op_key_off;
+  uint32_t* op_key_len;
+  uint32_t* mg_grant_off;    // [n_mgs+1]
 };
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
 hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans
 hipError_t launch_w2_emit(const W2Args& a, hipStream_t stream);
 hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reason, uint8_t* fail_op,
-                           hipStream_t stream);
+                           uint8_t* op_decision, uint32_t* op_g0, int64_t* op_ts, hipStream_t stream);
 
 hipError_t launch_verify(const LaunchArgs& a, hipStream_t stream);
 

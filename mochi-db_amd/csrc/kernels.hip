@@ -29,8 +29,7 @@ namespace mochi {
 __global__ __launch_bounds__(256) void k_grant_prep(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ goff,
                                                     const uint32_t* __restrict__ glen, uint32_t n,
                                                     uint32_t* __restrict__ digest /* [8][n] */,
-                                                    int64_t* __restrict__ ts_out, uint32_t* __restrict__ hash_at /* [n] abs off lo */,
-                                                    uint64_t* __restrict__ hash_off_out, uint32_t* __restrict__ hash_len_out,
+                                                    int64_t* __restrict__ ts_out, uint64_t* __restrict__ hash_off_out, uint32_t* __restrict__ hash_len_out,
                                                     uint8_t* __restrict__ flags) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -49,7 +48,6 @@ __global__ __launch_bounds__(256) void k_grant_prep(const uint8_t* __restrict__ 
   hash_off_out[i] = goff[i] + hoff;
   hash_len_out[i] = ok ? hlen : 0xFFFFFFFFu;
   flags[i] = ok ? MOCHI_GRANT_PARSED : 0;
-  (void)hash_at;
 }
 
 // ---------------------------------------------------------------------------
@@ -187,81 +185,245 @@ __device__ bool hash_matches(const uint8_t* __restrict__ blob, uint64_t off, uin
   return diff == 0;
 }
 
-__global__ __launch_bounds__(256) void k_tally(const uint32_t* __restrict__ cert_grant_off,
-                                               const uint32_t* __restrict__ cert_op_off,
-                                               const uint8_t* __restrict__ grant_key, const uint8_t* __restrict__ op_key,
-                                               const uint8_t* __restrict__ op_flags, const uint8_t* __restrict__ flags,
-                                               const int64_t* __restrict__ ts, const uint8_t* __restrict__ blob,
-                                               const uint64_t* __restrict__ hash_off, const uint32_t* __restrict__ hash_len,
-                                               const uint8_t* __restrict__ expected, uint32_t n_certs, uint32_t majority,
-                                               uint32_t strict_gt, uint32_t* __restrict__ accept_bits,
-                                               uint8_t* __restrict__ reason_out, uint8_t* __restrict__ fail_op_out) {
+// Everything k_tally reads, by value (one kernel argument block).
+struct TallyArgs {
+  const uint32_t* cert_grant_off;
+  const uint32_t* cert_op_off;
+  const uint32_t* cert_mg_off;   // null: a MultiGrant = a maximal run of equal signers
+  const uint32_t* mg_grant_off;
+  const uint8_t* grant_key;
+  const uint16_t* signer;
+  const uint8_t* op_key;
+  const uint8_t* op_flags;
+  const int64_t* op_object_ts;   // null: no stored certificates
+  const uint64_t* op_key_off;    // MOCHI_Q_BIND
+  const uint32_t* op_key_len;
+  const uint8_t* flags;
+  const int64_t* ts;
+  const uint8_t* blob;
+  const uint64_t* grant_off;
+  const uint32_t* grant_len;
+  const uint64_t* hash_off;
+  const uint32_t* hash_len;
+  const uint8_t* expected;
+  uint32_t n_certs, majority, strict_gt, quorum_mode;
+  uint32_t* accept_bits;
+  uint8_t* reason_out;
+  uint8_t* fail_op_out;
+  uint8_t* op_decision;
+  uint32_t* op_g0;
+  int64_t* op_ts;
+  const uint32_t* op_out_off;
+};
+
+// MOCHI_Q_BIND: Grant.objectId == the op key it is filed under (op `o`'s
+// operand1) and Grant.transactionHash == expected.
+__device__ bool grant_bound(const TallyArgs& a, uint32_t g, uint32_t o, const uint8_t* expected) {
+  if (!a.op_key_off || !a.op_key_len) return false;
+  ByteReader r;
+  r.init(a.blob + a.grant_off[g], a.grant_len[g]);
+  int64_t t;
+  uint32_t ho, hl, oo, ol;
+  if (!parse_grant(r, t, ho, hl, oo, ol)) return false;
+  const uint32_t kl = a.op_key_len[o];
+  if (ol != kl) return false;
+  const uint8_t* k = a.blob + a.op_key_off[o];
+  const uint8_t* id = a.blob + a.grant_off[g] + oo;
+#pragma unroll 1
+  for (uint32_t i = 0; i < kl; i++)
+    if (id[i] != k[i]) return false;
+  return hash_matches(a.blob, a.grant_off[g] + ho, hl, expected);
+}
+
+// Grant g counts toward its key slot's quorum list (reference parity: its
+// signature verified -- invalid => absent, InMemoryDataStore.java:622-624 --
+// and an op names its slot); MOCHI_Q_BIND / MOCHI_Q_DISTINCT_SIGNERS exclude
+// more.  first_op[] is not kept per lane: the op naming slot s is found by scan.
+__device__ bool counts(const TallyArgs& a, uint32_t g, uint32_t g_lo, uint32_t o_lo, uint32_t o_hi,
+                       const uint8_t* expected) {
+  if (!(a.flags[g] & MOCHI_GRANT_SIG_OK)) return false;
+  if (a.quorum_mode == 0) return true;  // callers only ask about slots an op names
+  const uint32_t s = a.grant_key[g];
+  uint32_t fo = 0xFFFFFFFFu;
+#pragma unroll 1
+  for (uint32_t o = o_lo; o < o_hi; o++)
+    if (a.op_key[o] == s) {
+      fo = o;
+      break;
+    }
+  if (fo == 0xFFFFFFFFu) return false;  // no op looks this key up
+  const bool bind = a.quorum_mode & MOCHI_Q_BIND;
+  if (bind && !grant_bound(a, g, fo, expected)) return false;
+  if (a.quorum_mode & MOCHI_Q_DISTINCT_SIGNERS) {
+    // the first grant of (slot, signer) that passes the other checks counts
+#pragma unroll 1
+    for (uint32_t q = g_lo; q < g; q++)
+      if (a.grant_key[q] == s && a.signer[q] == a.signer[g] && (a.flags[q] & MOCHI_GRANT_SIG_OK) &&
+          (!bind || grant_bound(a, q, fo, expected)))
+        return false;
+  }
+  return true;
+}
+
+// getCurrentTimestampFromCurrentCertificate on the INCOMING certificate
+// (StoreValueObjectContainer.java:175-198, called by applyOperation after
+// setCurrentC(wc), InMemoryDataStore.java:533-534): every MultiGrant must hold a
+// grant for the key, all with one timestamp.  Signatures play no part.
+__device__ bool incoming_cert_ok(const TallyArgs& a, uint32_t c, uint32_t g_lo, uint32_t g_hi, uint32_t s) {
+  bool have = false, ok = true;
+  int64_t t0 = 0;
+  if (a.cert_mg_off && a.mg_grant_off) {
+    const uint32_t m_lo = a.cert_mg_off[c], m_hi = a.cert_mg_off[c + 1];
+#pragma unroll 1
+    for (uint32_t m = m_lo; m < m_hi && ok; m++) {
+      bool found = false;
+#pragma unroll 1
+      for (uint32_t g = a.mg_grant_off[m]; g < a.mg_grant_off[m + 1]; g++) {
+        if (a.grant_key[g] != s) continue;
+        found = true;
+        const int64_t t = a.ts[g];
+        if (!have) {
+          have = true;
+          t0 = t;
+        } else if (t != t0) {
+          ok = false;
+        }
+      }
+      ok = ok && found;
+    }
+  } else {
+    bool found = true;  // vacuous before the first run
+#pragma unroll 1
+    for (uint32_t g = g_lo; g < g_hi && ok; g++) {
+      if (g == g_lo || a.signer[g] != a.signer[g - 1]) {  // a new MultiGrant starts
+        ok = found;
+        found = false;
+      }
+      if (a.grant_key[g] != s) continue;
+      found = true;
+      const int64_t t = a.ts[g];
+      if (!have) {
+        have = true;
+        t0 = t;
+      } else if (t != t0) {
+        ok = false;
+      }
+    }
+    ok = ok && found;
+  }
+  return ok && have;  // no MultiGrant at all: null Long unboxed (NPE)
+}
+
+// Certificate tally (lane = certificate).  Restates oracle_tally, i.e.
+// InMemoryDataStore.java:613-640 then write2apply :576-611 including the
+// read/apply step (:594-599, :521-574).
+__global__ __launch_bounds__(256) void k_tally(const TallyArgs a) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t reason = MOCHI_ACCEPT, fail_op = 0xFF;
-  if (c < n_certs) {
-    const uint32_t g_lo = cert_grant_off[c], g_hi = cert_grant_off[c + 1];
-    const uint32_t o_lo = cert_op_off[c], o_hi = cert_op_off[c + 1];
+  if (c < a.n_certs) {
+    const uint32_t g_lo = a.cert_grant_off[c], g_hi = a.cert_grant_off[c + 1];
+    const uint32_t o_lo = a.cert_op_off[c], o_hi = a.cert_op_off[c + 1];
+    const uint8_t* expected = a.expected + (size_t)c * MOCHI_TXN_HASH_BYTES;
     for (uint32_t g = g_lo; g < g_hi; g++)
-      if (!(flags[g] & MOCHI_GRANT_PARSED)) reason = MOCHI_REJECT_MALFORMED;
-    // processMultiGrantsFromAllServers: per named key slot, every valid grant's
-    // ts must equal the first valid grant's ts (wire order).
+      if (!(a.flags[g] & MOCHI_GRANT_PARSED)) reason = MOCHI_REJECT_MALFORMED;
+    // processMultiGrantsFromAllServers: per named key slot, every counted
+    // grant's ts must equal the first counted grant's ts (wire order).
     if (reason == MOCHI_ACCEPT) {
       for (uint32_t o = o_lo; o < o_hi && reason == MOCHI_ACCEPT; o++) {
-        const uint32_t s = op_key[o];
+        const uint32_t s = a.op_key[o];
         bool dup = false;
-        for (uint32_t q = o_lo; q < o; q++) dup |= op_key[q] == s;
+        for (uint32_t q = o_lo; q < o; q++) dup |= a.op_key[q] == s;
         if (dup) continue;
         bool seen = false;
         int64_t ts0 = 0;
         for (uint32_t g = g_lo; g < g_hi; g++) {
-          if (!(flags[g] & MOCHI_GRANT_SIG_OK) || grant_key[g] != s) continue;
+          if (a.grant_key[g] != s || !counts(a, g, g_lo, o_lo, o_hi, expected)) continue;
           if (!seen) {
             seen = true;
-            ts0 = ts[g];
-          } else if (ts[g] != ts0) {
+            ts0 = a.ts[g];
+          } else if (a.ts[g] != ts0) {
             reason = MOCHI_REJECT_TS_MISMATCH;
           }
         }
       }
     }
-    // write2apply verdict, ops in txn order
+    // write2apply, ops in txn order
+    uint64_t applied = 0, read = 0, wrong = 0;  // per-op decisions (<= 64 ops)
     if (reason == MOCHI_ACCEPT) {
       for (uint32_t o = o_lo; o < o_hi; o++) {
-        const uint32_t fl = op_flags[o];
-        if (!(fl & MOCHI_OP_LOCAL)) continue;
-        const uint32_t s = op_key[o];
+        const uint32_t j = o - o_lo;
+        const uint32_t fl = a.op_flags[o];
+        if (!(fl & MOCHI_OP_LOCAL)) {  // WRONG_SHARD  :582-587
+          wrong |= 1ull << j;
+          continue;
+        }
+        const uint32_t s = a.op_key[o];
         uint32_t mult = 0;
-        for (uint32_t q = o_lo; q < o_hi; q++) mult += op_key[q] == s;
+        bool applied_before = false;
+        for (uint32_t q = o_lo; q < o_hi; q++) {
+          mult += a.op_key[q] == s;
+          if (q < o && a.op_key[q] == s && ((applied >> (q - o_lo)) & 1)) applied_before = true;
+        }
         uint32_t valid = 0, first = 0xFFFFFFFFu;
         for (uint32_t g = g_lo; g < g_hi; g++) {
-          if (!(flags[g] & MOCHI_GRANT_SIG_OK) || grant_key[g] != s) continue;
+          if (a.grant_key[g] != s || !counts(a, g, g_lo, o_lo, o_hi, expected)) continue;
           if (first == 0xFFFFFFFFu) first = g;
           valid++;
         }
         const uint32_t cnt = valid * mult;
         uint32_t why = MOCHI_ACCEPT;
-        if (first == 0xFFFFFFFFu) why = MOCHI_REJECT_NO_GRANT;
-        else if (!(strict_gt ? cnt > majority : cnt >= majority)) why = MOCHI_REJECT_BELOW_QUORUM;
-        else if (!hash_matches(blob, hash_off[first], hash_len[first], expected + (size_t)c * MOCHI_TXN_HASH_BYTES))
-          why = MOCHI_REJECT_HASH_MISMATCH;
-        else if (!(fl & MOCHI_OP_HAS_SVOC)) why = MOCHI_REJECT_NO_SVOC;
+        if (first == 0xFFFFFFFFu) why = MOCHI_REJECT_NO_GRANT;                                      // :588
+        else if (!(a.strict_gt ? cnt > a.majority : cnt >= a.majority)) why = MOCHI_REJECT_BELOW_QUORUM;  // :590
+        else if (!hash_matches(a.blob, a.hash_off[first], a.hash_len[first], expected))
+          why = MOCHI_REJECT_HASH_MISMATCH;                                                       // :591,605-607
+        else if (!(fl & MOCHI_OP_HAS_SVOC)) why = MOCHI_REJECT_NO_SVOC;                           // :592-593
+        else {
+          // objectTS = svoc.getCurrentTimestampFromCurrentCertificate()  :594 (stored
+          // certificate: wc itself once an earlier op of this txn applied to the key)
+          const int64_t g0_ts = a.ts[first];
+          const bool has_cc = applied_before || (fl & MOCHI_OP_HAS_CURRENT_C);
+          const bool cc_bad = !applied_before && (fl & MOCHI_OP_CURRENT_C_BAD);
+          const int64_t obj_ts = applied_before ? g0_ts : (a.op_object_ts ? a.op_object_ts[o] : 0);
+          if (cc_bad) why = MOCHI_REJECT_STORED_CERT;
+          else if (fl & MOCHI_OP_NOT_WRITE) why = MOCHI_REJECT_NOT_WRITE;  // lock / action checks
+          else if (has_cc && obj_ts > g0_ts) read |= 1ull << j;            // readOperation  :596
+          else if (!incoming_cert_ok(a, c, g_lo, g_hi, s)) why = MOCHI_REJECT_APPLY_STATE;  // :533-534
+          else applied |= 1ull << j;                                        // applyOperation :597
+        }
         if (why != MOCHI_ACCEPT) {
           reason = why;
-          fail_op = o - o_lo;
+          fail_op = j;
           break;
         }
       }
     }
-    if (reason_out) reason_out[c] = (uint8_t)reason;
-    if (fail_op_out) fail_op_out[c] = (uint8_t)fail_op;
+    if (a.reason_out) a.reason_out[c] = (uint8_t)reason;
+    if (a.fail_op_out) a.fail_op_out[c] = (uint8_t)fail_op;
+    if (a.op_decision || a.op_g0 || a.op_ts) {
+      const uint32_t out0 = a.op_out_off ? a.op_out_off[c] : o_lo;
+      for (uint32_t o = o_lo; o < o_hi; o++) {
+        const uint32_t j = o - o_lo, s = a.op_key[o];
+        uint32_t first = 0xFFFFFFFFu;
+        for (uint32_t g = g_lo; g < g_hi && first == 0xFFFFFFFFu; g++)
+          if (a.grant_key[g] == s && counts(a, g, g_lo, o_lo, o_hi, expected)) first = g;
+        uint32_t d = MOCHI_OPD_SKIPPED;
+        if ((applied >> j) & 1) d = MOCHI_OPD_APPLY;
+        else if ((read >> j) & 1) d = MOCHI_OPD_READ;
+        else if ((wrong >> j) & 1) d = MOCHI_OPD_WRONG_SHARD;
+        else if (j == fail_op) d = MOCHI_OPD_FAILED;
+        if (a.op_decision) a.op_decision[out0 + j] = (uint8_t)d;
+        if (a.op_g0) a.op_g0[out0 + j] = first == 0xFFFFFFFFu ? first : first - g_lo;
+        if (a.op_ts) a.op_ts[out0 + j] = first == 0xFFFFFFFFu ? 0 : a.ts[first];
+      }
+    }
   }
   // accept bitmap: one ballot per wave covers 64 certificates = 2 words
-  const uint64_t acc = __ballot(c < n_certs && reason == MOCHI_ACCEPT);
+  const uint64_t acc = __ballot(c < a.n_certs && reason == MOCHI_ACCEPT);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wbase = (c - lane) >> 5;
-  const uint32_t nwords = (n_certs + 31) >> 5;
-  if (lane == 0 && wbase < nwords) accept_bits[wbase] = (uint32_t)acc;
-  if (lane == 0 && wbase + 1 < nwords) accept_bits[wbase + 1] = (uint32_t)(acc >> 32);
+  const uint32_t nwords = (a.n_certs + 31) >> 5;
+  if (lane == 0 && wbase < nwords) a.accept_bits[wbase] = (uint32_t)acc;
+  if (lane == 0 && wbase + 1 < nwords) a.accept_bits[wbase + 1] = (uint32_t)(acc >> 32);
 }
 
 __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t* __restrict__ flags, uint32_t n, uint8_t mask,
@@ -320,7 +482,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   mark(kStagePrep, false, ps);
   if (prep)
     hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, a.blob, a.grant_off, a.grant_len, N,
-                       a.digest, a.ts, nullptr, a.hash_off, a.hash_len, a.flags);
+                       a.digest, a.ts, a.hash_off, a.hash_len, a.flags);
   mark(kStagePrep, true, ps);
   if (fork) {
     hipError_t e = hipEventRecord(a.ev_join, a.aux);
@@ -342,10 +504,40 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   }
   mark(kStageFinal, true, st);
   mark(kStageTally, false, st);
-  if (C && !a.skip_prep_tally)
-    hipLaunchKernelGGL(k_tally, dim3(cdiv(C, 256)), dim3(256), 0, st, a.cert_grant_off, a.cert_op_off, a.grant_key,
-                       a.op_key, a.op_flags, a.flags, a.ts, a.blob, a.hash_off, a.hash_len, a.expected_hash, C,
-                       a.majority, a.strict_gt, a.cert_accept_bits, a.cert_reason, a.cert_fail_op);
+  if (C && !a.skip_prep_tally) {
+    TallyArgs t;
+    t.cert_grant_off = a.cert_grant_off;
+    t.cert_op_off = a.cert_op_off;
+    t.cert_mg_off = a.cert_mg_off;
+    t.mg_grant_off = a.mg_grant_off;
+    t.grant_key = a.grant_key;
+    t.signer = a.signer;
+    t.op_key = a.op_key;
+    t.op_flags = a.op_flags;
+    t.op_object_ts = a.op_object_ts;
+    t.op_key_off = a.op_key_off;
+    t.op_key_len = a.op_key_len;
+    t.flags = a.flags;
+    t.ts = a.ts;
+    t.blob = a.blob;
+    t.grant_off = a.grant_off;
+    t.grant_len = a.grant_len;
+    t.hash_off = a.hash_off;
+    t.hash_len = a.hash_len;
+    t.expected = a.expected_hash;
+    t.n_certs = C;
+    t.majority = a.majority;
+    t.strict_gt = a.strict_gt;
+    t.quorum_mode = a.quorum_mode;
+    t.accept_bits = a.cert_accept_bits;
+    t.reason_out = a.cert_reason;
+    t.fail_op_out = a.cert_fail_op;
+    t.op_decision = a.op_decision;
+    t.op_g0 = a.op_g0;
+    t.op_ts = a.op_ts;
+    t.op_out_off = a.op_out_off;
+    hipLaunchKernelGGL(k_tally, dim3(cdiv(C, 256)), dim3(256), 0, st, t);
+  }
   mark(kStageTally, true, st);
   return hipGetLastError();
 }

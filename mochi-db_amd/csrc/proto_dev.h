@@ -128,7 +128,8 @@ __device__ __forceinline__ bool rd_string(ByteReader& r, uint32_t& pos, uint32_t
   return true;
 }
 
-__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
+__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
+                                   uint32_t& oid_len) {
   uint32_t pos = 0;
   int64_t t = 0;
   uint32_t hoff = 0, hlen = 0, ooff = 0, olen = 0;
@@ -196,7 +197,14 @@ __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_of
   ts = t;
   hash_off = hoff;
   hash_len = hlen;
+  oid_off = ooff;
+  oid_len = olen;
   return true;
+}
+
+__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
+  uint32_t oo, ol;
+  return parse_grant(r, ts, hash_off, hash_len, oo, ol);
 }
 
 

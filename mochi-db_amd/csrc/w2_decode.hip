@@ -349,6 +349,17 @@ __device__ void last_string(ByteReader& r, uint32_t off, uint32_t len, uint32_t 
     }
 }
 
+// Last value of varint field `field` (wire type 0) of [off, off+len); 0 if absent.
+__device__ uint64_t last_varint(ByteReader& r, uint32_t off, uint32_t len, uint32_t field) {
+  uint64_t v = 0;
+  uint32_t pos = off, end = off + len;
+  Fld f;
+#pragma unroll 1
+  while (next_fld(r, pos, end, f) > 0)
+    if (f.field == field && f.wt == 0) v = f.v;
+  return v;
+}
+
 // Varint at [pos, end) is the minimal encoding of its value.
 __device__ bool canon_varint(ByteReader& r, uint32_t& pos, uint32_t end, uint64_t& v) {
   const uint32_t p0 = pos;
@@ -397,13 +408,17 @@ struct W2Out {
   uint8_t* grant_key;
   uint8_t* op_key;
   uint8_t* op_flags;
+  int64_t* op_object_ts;
+  uint64_t* op_key_off;
+  uint32_t* op_key_len;
+  uint32_t* mg_grant_off;
 };
 
 template <bool EMIT>
 __device__ uint32_t decode_msg(ByteReader& r, uint64_t msg_off, const uint8_t* __restrict__ ids,
                                const uint32_t* __restrict__ id_off, uint32_t n_ids, uint32_t& n_grants,
-                               uint32_t& n_ops, uint32_t g_base, uint32_t o_base, const uint8_t* flags_in,
-                               const W2Out& out) {
+                               uint32_t& n_ops, uint32_t& n_mgs, uint32_t g_base, uint32_t o_base, uint32_t m_base,
+                               const uint8_t* flags_in, const int64_t* ots_in, const W2Out& out) {
   uint32_t wc_off = 0, wc_len = 0, tx_off = 0, tx_len = 0, n_wc = 0, n_tx = 0;
   {
     uint32_t pos = 0;
@@ -448,8 +463,17 @@ __device__ uint32_t decode_msg(ByteReader& r, uint64_t msg_off, const uint8_t* _
           }
           j++;
         }
+        // Operation.action (enum, proto3 open): anything but WRITE = 2 / DELETE = 1
+        // fails applyOperation / readOperation (InMemoryDataStore.java:529, :562);
+        // an empty operand1 is never write-locked (:339-358)
+        const int32_t action = (int32_t)(uint32_t)last_varint(r, f.off, f.len, 1);
+        const uint32_t notw = (action != 1 && action != 2) || kl == 0 ? MOCHI_OP_NOT_WRITE : 0;
         out.op_key[o_base + no] = (uint8_t)slot;
-        out.op_flags[o_base + no] = flags_in ? flags_in[no] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
+        out.op_flags[o_base + no] =
+            (uint8_t)((flags_in ? flags_in[no] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC)) | notw);
+        out.op_object_ts[o_base + no] = ots_in ? ots_in[no] : 0;
+        out.op_key_off[o_base + no] = msg_off + ko;
+        out.op_key_len[o_base + no] = kl;
       }
       no++;
     }
@@ -460,6 +484,7 @@ __device__ uint32_t decode_msg(ByteReader& r, uint64_t msg_off, const uint8_t* _
   uint32_t status = MOCHI_MSG_OK;
   const bool ok = for_map(r, wc_off, wc_len, 1, [&](const Entry&, const Entry& mgv) -> bool {
     if (++n_mg > kMaxMG) return false;
+    if (EMIT) out.mg_grant_off[m_base + n_mg - 1] = g_base + ng;  // this MultiGrant's first grant
     const uint32_t mo = mgv.voff, ml = mgv.vlen;
     uint16_t signer = 0xFFFF;
     if (EMIT) {
@@ -527,6 +552,7 @@ __device__ uint32_t decode_msg(ByteReader& r, uint64_t msg_off, const uint8_t* _
   });
   if (!ok) status = MOCHI_MSG_FALLBACK;
   n_grants = ng;
+  n_mgs = n_mg;
   return status;
 }
 
@@ -553,27 +579,29 @@ __global__ __launch_bounds__(256) void k_w2_count(const uint8_t* __restrict__ wi
                                                   const uint32_t* __restrict__ flags_off,
                                                   const uint32_t* __restrict__ valid,
                                                   uint32_t* __restrict__ cnt_g, uint32_t* __restrict__ cnt_o,
-                                                  uint8_t* __restrict__ status) {
+                                                  uint32_t* __restrict__ cnt_m, uint8_t* __restrict__ status) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m > M) return;
   if (m == M) {  // the scan's extra element: totals land at [M]
     cnt_g[M] = 0;
     cnt_o[M] = 0;
+    cnt_m[M] = 0;
     return;
   }
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
-  uint32_t ng = 0, no = 0, st;
+  uint32_t ng = 0, no = 0, nm = 0, st;
   if (!valid[m]) {
     st = MOCHI_MSG_MALFORMED;
   } else {
     W2Out none{};
-    st = decode_msg<false>(r, moff[m], nullptr, nullptr, 0, ng, no, 0, 0, nullptr, none);
+    st = decode_msg<false>(r, moff[m], nullptr, nullptr, 0, ng, no, nm, 0, 0, 0, nullptr, nullptr, none);
     if (st == MOCHI_MSG_OK && flags_off && flags_off[m + 1] - flags_off[m] != no) st = MOCHI_MSG_OPS_MISMATCH;
   }
-  if (st != MOCHI_MSG_OK) ng = no = 0;
+  if (st != MOCHI_MSG_OK) ng = no = nm = 0;
   cnt_g[m] = ng;
   cnt_o[m] = no;
+  cnt_m[m] = nm;
   status[m] = (uint8_t)st;
 }
 
@@ -582,16 +610,20 @@ __global__ __launch_bounds__(256) void k_w2_emit(const uint8_t* __restrict__ wir
                                                  const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off,
                                                  uint32_t n_ids, const uint32_t* __restrict__ flags_off,
                                                  const uint8_t* __restrict__ flags_in,
+                                                 const int64_t* __restrict__ ots_in,
                                                  const uint32_t* __restrict__ g_base,
                                                  const uint32_t* __restrict__ o_base,
+                                                 const uint32_t* __restrict__ m_base,
                                                  const uint8_t* __restrict__ status, W2Out out) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m == 0) out.mg_grant_off[m_base[M]] = g_base[M];  // CSR terminator: n_mgs -> N
   if (m >= M || status[m] != MOCHI_MSG_OK) return;
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
-  uint32_t ng, no;
-  decode_msg<true>(r, moff[m], ids, id_off, n_ids, ng, no, g_base[m], o_base[m],
-                   flags_off ? flags_in + flags_off[m] : nullptr, out);
+  uint32_t ng, no, nm;
+  decode_msg<true>(r, moff[m], ids, id_off, n_ids, ng, no, nm, g_base[m], o_base[m], m_base[m],
+                   flags_off ? flags_in + flags_off[m] : nullptr,
+                   flags_off && ots_in ? ots_in + flags_off[m] : nullptr, out);
 }
 
 // sig[g] = wire[sig_src[g] .. +256) (zeros when absent): 16 lanes per grant,
@@ -618,13 +650,21 @@ __global__ __launch_bounds__(256) void k_w2_sig(const uint8_t* __restrict__ wire
 
 __global__ __launch_bounds__(256) void k_w2_fixup(const uint8_t* __restrict__ status, uint32_t M,
                                                   uint32_t* __restrict__ accept_bits, uint8_t* __restrict__ reason,
-                                                  uint8_t* __restrict__ fail_op) {
+                                                  uint8_t* __restrict__ fail_op, const uint32_t* __restrict__ op_out_off,
+                                                  uint8_t* __restrict__ op_decision, uint32_t* __restrict__ op_g0,
+                                                  int64_t* __restrict__ op_ts) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   const bool bad = m < M && status[m] != MOCHI_MSG_OK;
   const uint64_t badmask = __ballot(bad);
   if (m < M && bad) {
     if (reason) reason[m] = status[m] == MOCHI_MSG_MALFORMED ? MOCHI_REJECT_MALFORMED : MOCHI_UNDECIDED;
     if (fail_op) fail_op[m] = 0xFF;
+    if (op_out_off)  // ops of an undecoded message: not reached
+      for (uint32_t o = op_out_off[m]; o < op_out_off[m + 1]; o++) {
+        if (op_decision) op_decision[o] = MOCHI_OPD_SKIPPED;
+        if (op_g0) op_g0[o] = 0xFFFFFFFFu;
+        if (op_ts) op_ts[o] = 0;
+      }
   }
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wbase = (m - lane) >> 5, nwords = (M + 31) >> 5;
@@ -647,30 +687,34 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
     hipLaunchKernelGGL(k_w2_valid, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M,
                        a.cert_op_off);
   hipLaunchKernelGGL(k_w2_count, dim3(cdiv((uint64_t)a.M + 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len,
-                     a.M, a.flags_off, a.cert_op_off, a.cnt_g, a.cnt_o, a.status);
+                     a.M, a.flags_off, a.cert_op_off, a.cnt_g, a.cnt_o, a.cnt_m, a.status);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t tb = a.scan_temp_bytes;
   e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_g, a.cert_grant_off, (int)(a.M + 1), st);
   if (e != hipSuccess) return e;
   tb = a.scan_temp_bytes;
-  return hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_o, a.cert_op_off, (int)(a.M + 1), st);
+  e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_o, a.cert_op_off, (int)(a.M + 1), st);
+  if (e != hipSuccess) return e;
+  tb = a.scan_temp_bytes;
+  return hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_m, a.cert_mg_off, (int)(a.M + 1), st);
 }
 
 hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
-  W2Out o{a.sig_src, a.grant_off, a.grant_len, a.sig, a.signer, a.grant_key, a.op_key, a.op_flags};
-  if (a.M)
-    hipLaunchKernelGGL(k_w2_emit, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, a.ids,
-                       a.id_off, a.n_ids, a.flags_off, a.flags_in, a.cert_grant_off, a.cert_op_off, a.status, o);
+  W2Out o{a.sig_src, a.grant_off, a.grant_len, a.sig, a.signer, a.grant_key, a.op_key, a.op_flags,
+          a.op_object_ts, a.op_key_off, a.op_key_len, a.mg_grant_off};
+  hipLaunchKernelGGL(k_w2_emit, dim3(cdiv(a.M ? a.M : 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M,
+                     a.ids, a.id_off, a.n_ids, a.flags_off, a.flags_in, a.ots_in, a.cert_grant_off, a.cert_op_off,
+                     a.cert_mg_off, a.status, o);
   if (a.N) hipLaunchKernelGGL(k_w2_sig, dim3(cdiv((uint64_t)a.N * 16, 256)), dim3(256), 0, st, a.wire, a.sig_src, a.N, a.sig);
   return hipGetLastError();
 }
 
 hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reason, uint8_t* fail_op,
-                           hipStream_t st) {
+                           uint8_t* op_decision, uint32_t* op_g0, int64_t* op_ts, hipStream_t st) {
   if (a.M)
     hipLaunchKernelGGL(k_w2_fixup, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.status, a.M, accept_bits, reason,
-                       fail_op);
+                       fail_op, a.flags_off, op_decision, op_g0, op_ts);
   return hipGetLastError();
 }
 

@@ -40,6 +40,9 @@ REJECT_BELOW_QUORUM = 3
 REJECT_HASH_MISMATCH = 4
 REJECT_NO_SVOC = 5
 REJECT_MALFORMED = 6
+REJECT_APPLY_STATE = 8
+REJECT_STORED_CERT = 9
+REJECT_NOT_WRITE = 10
 REASON_NAMES = {
     ACCEPT: "ACCEPT",
     REJECT_TS_MISMATCH: "TS_MISMATCH",
@@ -48,10 +51,23 @@ REASON_NAMES = {
     REJECT_HASH_MISMATCH: "HASH_MISMATCH",
     REJECT_NO_SVOC: "NO_SVOC",
     REJECT_MALFORMED: "MALFORMED",
+    REJECT_APPLY_STATE: "APPLY_STATE",
+    REJECT_STORED_CERT: "STORED_CERT",
+    REJECT_NOT_WRITE: "NOT_WRITE",
 }
 
 OP_LOCAL = 0x01
 OP_HAS_SVOC = 0x02
+OP_HAS_CURRENT_C = 0x04
+OP_CURRENT_C_BAD = 0x08
+OP_NOT_WRITE = 0x10
+
+# per-op decisions (enum mochi_op_decision)
+OPD_SKIPPED, OPD_APPLY, OPD_READ, OPD_WRONG_SHARD, OPD_FAILED = 0, 1, 2, 3, 4
+
+# mochi_params.quorum_mode bits
+Q_DISTINCT_SIGNERS = 0x1
+Q_BIND = 0x2
 GRANT_SIG_OK = 0x01
 GRANT_PARSED = 0x02
 
@@ -65,7 +81,7 @@ class Batch_C(ctypes.Structure):
         ("n_grants", ctypes.c_uint32),
         ("n_certs", ctypes.c_uint32),
         ("n_ops", ctypes.c_uint32),
-        ("_pad0", ctypes.c_uint32),
+        ("n_mgs", ctypes.c_uint32),
         ("grant_bytes_len", ctypes.c_uint64),
         ("grant_bytes", ctypes.c_void_p),
         ("grant_off", ctypes.c_void_p),
@@ -78,6 +94,11 @@ class Batch_C(ctypes.Structure):
         ("op_key", ctypes.c_void_p),
         ("op_flags", ctypes.c_void_p),
         ("expected_hash", ctypes.c_void_p),
+        ("cert_mg_off", ctypes.c_void_p),
+        ("mg_grant_off", ctypes.c_void_p),
+        ("op_object_ts", ctypes.c_void_p),
+        ("op_key_off", ctypes.c_void_p),
+        ("op_key_len", ctypes.c_void_p),
     ]
 
 
@@ -85,8 +106,13 @@ class Params_C(ctypes.Structure):
     _fields_ = [
         ("replication_factor", ctypes.c_uint32),
         ("strict_gt", ctypes.c_uint32),
-        ("_pad", ctypes.c_uint32 * 2),
+        ("quorum_mode", ctypes.c_uint32),
+        ("_pad", ctypes.c_uint32),
     ]
+
+
+def params(replication_factor: int, strict_gt: bool = True, quorum_mode: int = 0) -> "Params_C":
+    return Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0, quorum_mode=quorum_mode)
 
 
 class Verdicts_C(ctypes.Structure):
@@ -97,10 +123,14 @@ class Verdicts_C(ctypes.Structure):
         ("cert_accept_bits", ctypes.c_void_p),
         ("cert_reason", ctypes.c_void_p),
         ("cert_fail_op", ctypes.c_void_p),
+        ("op_decision", ctypes.c_void_p),
+        ("op_g0", ctypes.c_void_p),
+        ("op_ts", ctypes.c_void_p),
     ]
 
 
 _lib = None
+ABI_VERSION = 2
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -159,7 +189,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_host_alloc.restype = vp
     lib.mochi_host_alloc.argtypes = [ctypes.c_uint64]
     lib.mochi_host_free.argtypes = [vp]
-    if lib.mochi_abi_version() != 1:
+    if lib.mochi_abi_version() != ABI_VERSION:
         raise MochiError("libmochi_hip ABI mismatch")
     _lib = lib
     return lib
@@ -192,6 +222,22 @@ class Batch:
     op_key: np.ndarray  # uint8 [O]
     op_flags: np.ndarray  # uint8 [O]
     expected_hash: np.ndarray  # uint8 [C, 128]
+    # ABI 2 (optional): MultiGrant CSR, stored-certificate timestamps, op key slices
+    cert_mg_off: Optional[np.ndarray] = None  # uint32 [C+1]
+    mg_grant_off: Optional[np.ndarray] = None  # uint32 [n_mgs+1]
+    op_object_ts: Optional[np.ndarray] = None  # int64 [O]
+    op_key_off: Optional[np.ndarray] = None  # uint64 [O] into grant_bytes
+    op_key_len: Optional[np.ndarray] = None  # uint32 [O]
+
+    OPTIONAL = ("cert_mg_off", "mg_grant_off", "op_object_ts", "op_key_off", "op_key_len")
+    OPT_DTYPES = {"cert_mg_off": np.uint32, "mg_grant_off": np.uint32, "op_object_ts": np.int64,
+                  "op_key_off": np.uint64, "op_key_len": np.uint32}
+    FIELDS = ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off",
+              "cert_op_off", "op_key", "op_flags", "expected_hash")
+
+    @property
+    def n_mgs(self) -> int:
+        return 0 if self.mg_grant_off is None else int(self.mg_grant_off.shape[0]) - 1
 
     @property
     def n_grants(self) -> int:
@@ -218,14 +264,15 @@ class Batch:
             op_key=np.ascontiguousarray(self.op_key, dtype=np.uint8),
             op_flags=np.ascontiguousarray(self.op_flags, dtype=np.uint8),
             expected_hash=np.ascontiguousarray(self.expected_hash, dtype=np.uint8).reshape(-1, TXN_HASH_BYTES),
+            **{k: (None if getattr(self, k) is None else np.ascontiguousarray(getattr(self, k), dtype=self.OPT_DTYPES[k]))
+               for k in self.OPTIONAL},
         )
 
     def pinned(self) -> "Batch":
         """A copy whose arrays live in one pinned host allocation (mochi_host_alloc):
         mochi_verify_batch DMAs such arrays in place instead of staging them."""
         b = self.normalized()
-        names = ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off",
-                 "cert_op_off", "op_key", "op_flags", "expected_hash")
+        names = self.FIELDS + tuple(k for k in self.OPTIONAL if getattr(b, k) is not None)
         arrs = [getattr(b, nm) for nm in names]
         offs, total = [], 0
         for a in arrs:
@@ -256,6 +303,9 @@ class Batch:
         b.op_key = _ptr(self.op_key)
         b.op_flags = _ptr(self.op_flags)
         b.expected_hash = _ptr(self.expected_hash)
+        b.n_mgs = self.n_mgs
+        for k in self.OPTIONAL:
+            setattr(b, k, _ptr(getattr(self, k)))
         return b
 
 
@@ -286,10 +336,13 @@ class Verdicts:
     cert_accept_bits: np.ndarray
     cert_reason: np.ndarray
     cert_fail_op: np.ndarray
+    op_decision: Optional[np.ndarray] = None  # uint8 [O]
+    op_g0: Optional[np.ndarray] = None  # uint32 [O]
+    op_ts: Optional[np.ndarray] = None  # int64 [O]
     timing_ms: dict = field(default_factory=dict)
 
     @staticmethod
-    def alloc(n_grants: int, n_certs: int) -> "Verdicts":
+    def alloc(n_grants: int, n_certs: int, n_ops: int = 0) -> "Verdicts":
         return Verdicts(
             grant_valid_bits=np.zeros((n_grants + 31) // 32, np.uint32),
             grant_flags=np.zeros(n_grants, np.uint8),
@@ -297,6 +350,9 @@ class Verdicts:
             cert_accept_bits=np.zeros((n_certs + 31) // 32, np.uint32),
             cert_reason=np.zeros(n_certs, np.uint8),
             cert_fail_op=np.zeros(n_certs, np.uint8),
+            op_decision=np.full(n_ops, 0xEE, np.uint8),
+            op_g0=np.zeros(n_ops, np.uint32),
+            op_ts=np.zeros(n_ops, np.int64),
         )
 
     def to_c(self) -> Verdicts_C:
@@ -307,6 +363,10 @@ class Verdicts:
         v.cert_accept_bits = _ptr(self.cert_accept_bits)
         v.cert_reason = _ptr(self.cert_reason)
         v.cert_fail_op = _ptr(self.cert_fail_op)
+        # zero-length op arrays still get a pointer (n_ops == 0 reads nothing)
+        v.op_decision = _ptr(self.op_decision)
+        v.op_g0 = _ptr(self.op_g0)
+        v.op_ts = _ptr(self.op_ts)
         return v
 
     @property
@@ -360,15 +420,20 @@ class Verifier:
         if self.lib.mochi_ctx_set_server_ids(self.ctx, _ptr(blob), _ptr(off), len(enc)) != OK:
             raise MochiError(f"mochi_ctx_set_server_ids: {_err(self.lib)}")
 
-    def verify_write2(self, wb, replication_factor: int, strict_gt: bool = True):
+    def verify_write2(self, wb, replication_factor: int, strict_gt: bool = True, quorum_mode: int = 0):
         """Write2ToServer messages (workload.WireBatch, host memory) -> (Verdicts with
-        certificate-level arrays, msg_status[M])."""
+        certificate-level arrays -- and per-op arrays when wb.op_flags_off is set --,
+        msg_status[M])."""
         wc, keep = write2_batch_c(wb)
         M = wb.n_msgs
-        out = Verdicts.alloc(0, M)
+        O = int(wb.op_flags_off[-1]) if wb.op_flags_off is not None else 0
+        out = Verdicts.alloc(0, M, O)
         vc = out.to_c()
         vc.grant_valid_bits = vc.grant_flags = vc.grant_ts = None
-        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        if wb.op_flags_off is None:
+            vc.op_decision = vc.op_g0 = vc.op_ts = None
+            out.op_decision = out.op_g0 = out.op_ts = None
+        p = params(replication_factor, strict_gt, quorum_mode)
         st = np.zeros(max(M, 1), np.uint8)
         rc = self.lib.mochi_verify_write2(self.ctx, ctypes.addressof(wc), ctypes.addressof(p), ctypes.addressof(vc),
                                           _ptr(st))
@@ -380,13 +445,15 @@ class Verifier:
         return out, st[:M].copy()
 
     def verify_write2_device(self, dwb: "DeviceWireBatch", out: "DeviceVerdicts", replication_factor: int,
-                             strict_gt: bool = True, stream: int = 0) -> None:
+                             strict_gt: bool = True, stream: int = 0, quorum_mode: int = 0) -> None:
         """Device-resident Write2 wire messages -> certificate verdicts (async on `stream`,
         except for one wait on the decoded grant / op totals)."""
         wc = dwb.to_c()
         vc = out.to_c()
         vc.grant_valid_bits = vc.grant_flags = vc.grant_ts = None
-        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        if dwb.op_flags_off is None:
+            vc.op_decision = vc.op_g0 = vc.op_ts = None
+        p = params(replication_factor, strict_gt, quorum_mode)
         rc = self.lib.mochi_verify_write2_device(self.ctx, ctypes.addressof(wc), ctypes.addressof(p),
                                                  ctypes.addressof(vc), dwb.status.data_ptr(), stream)
         if rc != OK:
@@ -411,7 +478,10 @@ class Verifier:
                    sig=arr(d.sig, N * 256, np.uint8).reshape(N, 256), signer=arr(d.signer, N, np.uint16),
                    grant_key=arr(d.grant_key, N, np.uint8), cert_grant_off=arr(d.cert_grant_off, M + 1, np.uint32),
                    cert_op_off=arr(d.cert_op_off, M + 1, np.uint32), op_key=arr(d.op_key, O, np.uint8),
-                   op_flags=arr(d.op_flags, O, np.uint8), msg_status=arr(d.msg_status, M, np.uint8))
+                   op_flags=arr(d.op_flags, O, np.uint8), msg_status=arr(d.msg_status, M, np.uint8),
+                   cert_mg_off=arr(d.cert_mg_off, M + 1, np.uint32),
+                   mg_grant_off=arr(d.mg_grant_off, d.n_mgs + 1, np.uint32),
+                   op_key_off=arr(d.op_key_off, O, np.uint64), op_key_len=arr(d.op_key_len, O, np.uint32))
         self.lib.mochi_write2_decoded_free(ctypes.addressof(d))
         return out
 
@@ -431,12 +501,12 @@ class Verifier:
         except Exception:
             pass
 
-    def verify(self, batch: Batch, replication_factor: int, strict_gt: bool = True) -> Verdicts:
+    def verify(self, batch: Batch, replication_factor: int, strict_gt: bool = True, quorum_mode: int = 0) -> Verdicts:
         """Host-memory batch -> verdicts (pinned staging, synchronous)."""
         b = batch.normalized()
-        out = Verdicts.alloc(b.n_grants, b.n_certs)
+        out = Verdicts.alloc(b.n_grants, b.n_certs, b.n_ops)
         bc, vc = b.to_c(), out.to_c()
-        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        p = params(replication_factor, strict_gt, quorum_mode)
         rc = self.lib.mochi_verify_batch(self.ctx, ctypes.byref(bc), ctypes.byref(p), ctypes.byref(vc))
         if rc != OK:
             raise MochiError(f"mochi_verify_batch rc={rc}: {_err(self.lib)}")
@@ -464,9 +534,9 @@ class Verifier:
         return out
 
     def verify_device(self, dev: "DeviceBatch", out: "DeviceVerdicts", replication_factor: int,
-                      strict_gt: bool = True, stream: int = 0) -> None:
+                      strict_gt: bool = True, stream: int = 0, quorum_mode: int = 0) -> None:
         """Device-resident batch (torch tensors) -> device verdicts; async on `stream`."""
-        p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        p = params(replication_factor, strict_gt, quorum_mode)
         bc, vc = dev.to_c(), out.to_c()
         rc = self.lib.mochi_verify_batch_device(self.ctx, ctypes.byref(bc), ctypes.byref(p), ctypes.byref(vc),
                                                 stream or None)
@@ -512,14 +582,21 @@ class DeviceBatch:
         self.op_key = t(b.op_key)
         self.op_flags = t(b.op_flags)
         self.expected_hash = t(b.expected_hash)
+        self.n_mgs = b.n_mgs
+        sv = {np.uint32: np.int32, np.uint64: np.int64, np.int64: np.int64}
+        for k in Batch.OPTIONAL:
+            a = getattr(b, k)
+            setattr(self, k, None if a is None else t(a.view(sv[Batch.OPT_DTYPES[k]])))
 
     def to_c(self) -> Batch_C:
         b = Batch_C()
-        b.n_grants, b.n_certs, b.n_ops = self.n_grants, self.n_certs, self.n_ops
+        b.n_grants, b.n_certs, b.n_ops, b.n_mgs = self.n_grants, self.n_certs, self.n_ops, self.n_mgs
         b.grant_bytes_len = int(self.grant_bytes.numel())
-        for name in ("grant_bytes", "grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off",
-                     "cert_op_off", "op_key", "op_flags", "expected_hash"):
+        for name in Batch.FIELDS:
             setattr(b, name, getattr(self, name).data_ptr())
+        for name in Batch.OPTIONAL:
+            a = getattr(self, name)
+            setattr(b, name, None if a is None else a.data_ptr())
         return b
 
 
@@ -538,6 +615,8 @@ class DeviceWireBatch:
         self.op_flags_off = None if wb.op_flags_off is None else t(np.ascontiguousarray(wb.op_flags_off, np.uint32).view(np.int32))
         self.op_flags = t(wb.op_flags if wb.op_flags.size else np.zeros(1, np.uint8))
         self.expected_hash = t(np.ascontiguousarray(wb.expected_hash, np.uint8).reshape(-1))
+        ots = getattr(wb, "op_object_ts", None)
+        self.op_object_ts = None if ots is None or wb.op_flags_off is None else t(np.ascontiguousarray(ots, np.int64))
         self.status = torch.zeros(max(self.n_msgs, 1), dtype=torch.uint8, device=dev)
 
     def to_c(self) -> "Write2Batch_C":
@@ -547,11 +626,12 @@ class DeviceWireBatch:
         c.wire, c.msg_off, c.msg_len = self.wire.data_ptr(), self.msg_off.data_ptr(), self.msg_len.data_ptr()
         c.op_flags_off = None if self.op_flags_off is None else self.op_flags_off.data_ptr()
         c.op_flags, c.expected_hash = self.op_flags.data_ptr(), self.expected_hash.data_ptr()
+        c.op_object_ts = None if self.op_object_ts is None else self.op_object_ts.data_ptr()
         return c
 
 
 class DeviceVerdicts:
-    def __init__(self, n_grants: int, n_certs: int, device: int = 0, full: bool = True):
+    def __init__(self, n_grants: int, n_certs: int, device: int = 0, full: bool = True, n_ops: int = 0):
         import torch
 
         dev = torch.device("cuda", device)
@@ -562,10 +642,17 @@ class DeviceVerdicts:
         self.grant_ts = torch.zeros(n_grants, dtype=torch.int64, device=dev) if full else None
         self.cert_reason = torch.zeros(n_certs, dtype=torch.uint8, device=dev) if full else None
         self.cert_fail_op = torch.zeros(n_certs, dtype=torch.uint8, device=dev) if full else None
+        op = full and n_ops > 0
+        self.op_decision = torch.zeros(n_ops, dtype=torch.uint8, device=dev) if op else None
+        self.op_g0 = torch.zeros(n_ops, dtype=torch.int32, device=dev) if op else None
+        self.op_ts = torch.zeros(n_ops, dtype=torch.int64, device=dev) if op else None
+
+    NAMES = ("grant_valid_bits", "grant_flags", "grant_ts", "cert_accept_bits", "cert_reason", "cert_fail_op",
+             "op_decision", "op_g0", "op_ts")
 
     def to_c(self) -> Verdicts_C:
         v = Verdicts_C()
-        for name in ("grant_valid_bits", "grant_flags", "grant_ts", "cert_accept_bits", "cert_reason", "cert_fail_op"):
+        for name in self.NAMES:
             t = getattr(self, name)
             setattr(v, name, t.data_ptr() if t is not None else None)
         return v
@@ -581,6 +668,9 @@ class DeviceVerdicts:
             cert_accept_bits=h(self.cert_accept_bits, np.uint32),
             cert_reason=h(self.cert_reason, np.uint8),
             cert_fail_op=h(self.cert_fail_op, np.uint8),
+            op_decision=h(self.op_decision, np.uint8),
+            op_g0=h(self.op_g0, np.uint32),
+            op_ts=h(self.op_ts, np.int64),
         )
 
 
@@ -692,6 +782,7 @@ class Write2Batch_C(ctypes.Structure):
         ("op_flags_off", ctypes.c_void_p),
         ("op_flags", ctypes.c_void_p),
         ("expected_hash", ctypes.c_void_p),
+        ("op_object_ts", ctypes.c_void_p),
     ]
 
 
@@ -707,20 +798,24 @@ def write2_batch_c(wb):
             None if wb.op_flags_off is None else np.ascontiguousarray(wb.op_flags_off, np.uint32),
             np.ascontiguousarray(wb.op_flags if wb.op_flags.size else np.zeros(1, np.uint8), np.uint8),
             np.ascontiguousarray(wb.expected_hash, np.uint8).reshape(-1)]
+    ots = getattr(wb, "op_object_ts", None)
+    arrs.append(None if ots is None or wb.op_flags_off is None else np.ascontiguousarray(ots, np.int64))
     c = Write2Batch_C()
     c.n_msgs = int(arrs[1].shape[0])
     c.wire_len = int(arrs[0].nbytes)
     c.wire, c.msg_off, c.msg_len = _ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2])
     c.op_flags_off, c.op_flags, c.expected_hash = _ptr(arrs[3]), _ptr(arrs[4]), _ptr(arrs[5])
+    c.op_object_ts = _ptr(arrs[6])
     return c, arrs
 
 
 class Write2Decoded_C(ctypes.Structure):
     _fields_ = [("n_msgs", ctypes.c_uint32), ("n_grants", ctypes.c_uint32), ("n_ops", ctypes.c_uint32),
-                ("_pad0", ctypes.c_uint32), ("grant_off", ctypes.c_void_p), ("grant_len", ctypes.c_void_p),
+                ("n_mgs", ctypes.c_uint32), ("grant_off", ctypes.c_void_p), ("grant_len", ctypes.c_void_p),
                 ("sig", ctypes.c_void_p), ("signer", ctypes.c_void_p), ("grant_key", ctypes.c_void_p),
                 ("cert_grant_off", ctypes.c_void_p), ("cert_op_off", ctypes.c_void_p), ("op_key", ctypes.c_void_p),
-                ("op_flags", ctypes.c_void_p), ("msg_status", ctypes.c_void_p)]
+                ("op_flags", ctypes.c_void_p), ("msg_status", ctypes.c_void_p), ("cert_mg_off", ctypes.c_void_p),
+                ("mg_grant_off", ctypes.c_void_p), ("op_key_off", ctypes.c_void_p), ("op_key_len", ctypes.c_void_p)]
 
 
 class Verdict1_C(ctypes.Structure):
@@ -736,7 +831,7 @@ class Batcher:
                  max_wait_us: int = 200, with_op_flags: bool = False):
         self.lib = verifier.lib
         self._ver = verifier
-        self._p = Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+        self._p = params(replication_factor, strict_gt)
         self.with_op_flags = with_op_flags
         self.h = self.lib.mochi_batcher_create(verifier.ctx, ctypes.addressof(self._p), max_msgs, max_wait_us,
                                                1 if with_op_flags else 0)

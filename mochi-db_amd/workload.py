@@ -329,6 +329,7 @@ class WireBatch:
     op_flags_off: Optional[np.ndarray]  # uint32 [M+1] or None
     op_flags: np.ndarray  # uint8
     expected_hash: np.ndarray  # uint8 [M, 128]
+    op_object_ts: Optional[np.ndarray] = None  # int64, aligned with op_flags (stored currentC timestamps)
 
     @property
     def n_msgs(self) -> int:
@@ -396,6 +397,59 @@ def server_id_table(n: int, server_ids=None):
     return np.frombuffer(blob, np.uint8).copy(), off
 
 
+def _txn_hashes(cidx: np.ndarray, suffix: str = "") -> np.ndarray:
+    """[C, 128] lowercase-hex SHA-512 of "txn-{c}{suffix}" (the objectSHA512 stand-in)."""
+    h = b"".join([hashlib.sha512(f"txn-{int(c)}{suffix}".encode()).hexdigest().encode() for c in cidx])
+    return np.frombuffer(h, np.uint8).reshape(-1, TXN_HASH_BYTES) if len(cidx) else np.zeros((0, 128), np.uint8)
+
+
+_OIDS = [f"DEMO_KEY_STRESS_TEST_{i}".encode() for i in range(200)]
+
+
+def encode_grants_vec(oid_idx: np.ndarray, ts: np.ndarray, hashes: np.ndarray) -> tuple:
+    """Vectorized Grant.toByteArray() (MochiProtocol.java:7556-7574) of n grants with
+    objectId DEMO_KEY_STRESS_TEST_{oid_idx}, timestamp ts (0 <= ts < 2^21; 0 is
+    omitted, proto3 default) and transactionHash = hashes[i] (128 ASCII bytes).
+    Returns (blob, offsets, lengths): the grants concatenated in input order."""
+    n = int(oid_idx.shape[0])
+    ts = np.asarray(ts, np.int64)
+    assert n == 0 or (ts.min() >= 0 and ts.max() < (1 << 21))
+    lo = np.array([len(x) for x in _OIDS], np.int64)[oid_idx]
+    lv = np.where(ts == 0, 0, np.where(ts < 128, 1, np.where(ts < 16384, 2, 3)))
+    ln = 2 + lo + np.where(lv > 0, 1 + lv, 0) + 3 + TXN_HASH_BYTES
+    W_ = int(ln.max()) if n else 0
+    rows = np.zeros((n, W_), np.uint8)
+    rows[:, 0] = 0x0A
+    rows[:, 1] = lo
+    otab = np.zeros((200, 24), np.uint8)
+    for i, x in enumerate(_OIDS):
+        otab[i, :len(x)] = np.frombuffer(x, np.uint8)
+    for L in np.unique(lo):
+        for v in np.unique(lv):
+            sel = np.nonzero((lo == L) & (lv == v))[0]
+            if not sel.size:
+                continue
+            L, v = int(L), int(v)
+            rows[sel, 2:2 + L] = otab[oid_idx[sel], :L]
+            p = 2 + L
+            if v:
+                t = ts[sel]
+                rows[sel, p] = 0x10
+                for b in range(v):
+                    byte = (t >> (7 * b)) & 0x7F
+                    rows[sel, p + 1 + b] = (byte | (0x80 if b + 1 < v else 0)).astype(np.uint8)
+                p += 1 + v
+            rows[sel, p] = 0x22
+            rows[sel, p + 1] = 0x80
+            rows[sel, p + 2] = 0x01
+            rows[sel, p + 3:p + 3 + TXN_HASH_BYTES] = hashes[sel]
+    blob = rows[np.arange(W_)[None, :] < ln[:, None]]
+    off = np.zeros(n, np.uint64)
+    if n:
+        np.cumsum(ln[:-1], out=off[1:])
+    return np.ascontiguousarray(blob), off, ln.astype(np.uint32)
+
+
 # ---------------------------------------------------------------------------
 # SURVEY.md §8d's per-certificate stream with UNIQUE grant bytes, signed on the
 # device (k_rsa_sign, bit-identical to OpenSSL): certificate c has objectId
@@ -425,47 +479,48 @@ def make_batch_unique(R: int, n_certs: int, k: int = 1, first_cert: int = 0, see
     rf[fault == FAULT_G0_HASH] = 0
     rf[fault == FAULT_G1_HASH] = 1 % R
     hts = (_h(seed, 7, cidx) % np.uint64(1000)).astype(np.int64)
+    ts_c = 1000 * (cidx % np.uint64(64)).astype(np.int64) + hts
+    expected = _txn_hashes(cidx)
     # grant bytes, certificate order: per op j the normal grant, then the faulty replica's variant
-    parts, pos = [], 0
-    off_norm = np.zeros((C, k), np.uint64)
-    len_norm = np.zeros((C, k), np.uint32)
-    off_var = np.zeros((C, k), np.uint64)
-    len_var = np.zeros((C, k), np.uint32)
-    expected = np.zeros((C, TXN_HASH_BYTES), np.uint8)
-    for i in range(C):
-        c = int(cidx[i])
-        th = hashlib.sha512(f"txn-{c}".encode()).hexdigest()
-        expected[i] = np.frombuffer(th.encode(), np.uint8)
-        ts = 1000 * (c % 64) + int(hts[i])
-        f = fault[i]
-        for j in range(k):
-            oid = f"DEMO_KEY_STRESS_TEST_{(c * k + j) % 200}"
-            g = encode_grant(oid, ts, th)
-            off_norm[i, j], len_norm[i, j] = pos, len(g)
-            parts.append(g)
-            pos += len(g)
-            if f == FAULT_TS or f == FAULT_G0_HASH or f == FAULT_G1_HASH:
-                v = encode_grant(oid, ts + 1, th) if f == FAULT_TS else \
-                    encode_grant(oid, ts, hashlib.sha512(f"txn-{c}-evil".encode()).hexdigest())
-                off_var[i, j], len_var[i, j] = pos, len(v)
-                parts.append(v)
-                pos += len(v)
-    blob = np.frombuffer(b"".join(parts), np.uint8).copy()
+    has_var = (fault == FAULT_TS) | (fault == FAULT_G0_HASH) | (fault == FAULT_G1_HASH)
+    nv = np.where(has_var, 2, 1)  # grant copies per (cert, op)
+    per_c = nv * k
+    start = np.zeros(C + 1, np.int64)
+    np.cumsum(per_c, out=start[1:])
+    tot = int(start[-1])
+    rep_c = np.repeat(np.arange(C), per_c)  # owning cert of each copy
+    within = np.arange(tot) - start[rep_c]
+    j_of = within // nv[rep_c]
+    var_of = within % nv[rep_c]  # 0 normal, 1 fault variant
+    oid_idx = ((cidx[rep_c].astype(np.int64) * k + j_of) % 200).astype(np.int64)
+    tsv = ts_c[rep_c] + np.where((var_of == 1) & (fault[rep_c] == FAULT_TS), 1, 0)
+    hashes = expected[rep_c]
+    evil_c = np.nonzero((fault == FAULT_G0_HASH) | (fault == FAULT_G1_HASH))[0]
+    if evil_c.size:
+        evil = _txn_hashes(cidx[evil_c], "-evil")
+        emap = np.full(C, -1, np.int64)
+        emap[evil_c] = np.arange(evil_c.size)
+        sel = np.nonzero((var_of == 1) & (emap[rep_c] >= 0))[0]
+        hashes[sel] = evil[emap[rep_c[sel]]]
+    blob, coff, clen = encode_grants_vec(oid_idx, tsv, hashes)
+    copy_at = lambda c, j, v: start[c] + j * nv[c] + v  # index of a grant copy
     # grid [C, R, k] -> kept grants in (certificate, replica, op) order
     shape = (C, R, k)
     rr = np.arange(R)[None, :, None]
     is_rf = np.broadcast_to(rr == rf[:, None, None], shape)
     f3 = np.broadcast_to(fault[:, None, None], shape)
-    use_var = ((f3 == FAULT_TS) | (f3 == FAULT_G0_HASH) | (f3 == FAULT_G1_HASH)) & is_rf
+    use_var = (has_var[:, None, None] & is_rf)
     keep = np.ones(shape, bool)
     keep[(f3 == FAULT_DROP) & is_rf] = False
-    goff_g = np.where(use_var, off_var[:, None, :], off_norm[:, None, :])
-    glen_g = np.where(use_var, len_var[:, None, :], len_norm[:, None, :])
+    C3 = np.broadcast_to(np.arange(C)[:, None, None], shape)
+    J3 = np.broadcast_to(np.arange(k)[None, None, :], shape)
     sel = keep.reshape(-1)
-    goff = np.broadcast_to(goff_g, shape).reshape(-1)[sel].astype(np.uint64)
-    glen = np.broadcast_to(glen_g, shape).reshape(-1)[sel].astype(np.uint32)
+    ci, ji, vi = C3.reshape(-1)[sel], J3.reshape(-1)[sel], use_var.reshape(-1)[sel].astype(np.int64)
+    gi = copy_at(ci, ji, vi)
+    goff = coff[gi]
+    glen = clen[gi]
     signer = np.broadcast_to(rr, shape).reshape(-1)[sel].astype(np.uint16)
-    gkey = np.broadcast_to(np.arange(k)[None, None, :], shape).reshape(-1)[sel].astype(np.uint8)
+    gkey = ji.astype(np.uint8)
     n = goff.shape[0]
     sig = np.zeros((n, RSA_BYTES), np.uint8)
     for r in range(R):
@@ -479,10 +534,10 @@ def make_batch_unique(R: int, n_certs: int, k: int = 1, first_cert: int = 0, see
     flags = np.full(n, 0x03, np.uint8)
     flip_c = np.nonzero(fault == FAULT_FLIP)[0]
     if flip_c.size:
-        gi = cert_grant_off[flip_c].astype(np.int64) + rf[flip_c] * k
+        gf = cert_grant_off[flip_c].astype(np.int64) + rf[flip_c] * k
         bit = (_h(seed, 4, cidx[flip_c]) % np.uint64(2048)).astype(np.int64)
-        sig[gi, bit // 8] ^= (1 << (bit % 8)).astype(np.uint8)
-        flags[gi] = 0x02
+        sig[gf, bit // 8] ^= (1 << (bit % 8)).astype(np.uint8)
+        flags[gf] = 0x02
     batch = Batch(grant_bytes=blob, grant_off=goff, grant_len=glen, sig=sig, signer=signer, grant_key=gkey,
                   cert_grant_off=cert_grant_off,
                   cert_op_off=(np.arange(C + 1, dtype=np.uint64) * k).astype(np.uint32),

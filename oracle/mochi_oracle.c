@@ -461,37 +461,128 @@ static int hash_equals(const uint8_t* g, uint32_t glen, const uint8_t expected[M
   return v.txn_hash_len == MOCHI_TXN_HASH_BYTES && memcmp(g + v.txn_hash_off, expected, MOCHI_TXN_HASH_BYTES) == 0;
 }
 
+/* MOCHI_Q_BIND: Grant.objectId == the op key it is filed under, and
+ * Grant.transactionHash == objectSHA512(txn). */
+static int grant_bound(const mochi_batch* b, uint32_t g, uint32_t op, const uint8_t* expected) {
+  oracle_grant_view v;
+  const uint8_t* gb = b->grant_bytes + b->grant_off[g];
+  if (!oracle_grant_parse(gb, b->grant_len[g], &v)) return 0;
+  if (!b->op_key_off || !b->op_key_len) return 0;
+  const uint32_t kl = b->op_key_len[op];
+  if (v.object_id_len != kl || memcmp(gb + v.object_id_off, b->grant_bytes + b->op_key_off[op], kl) != 0) return 0;
+  return hash_equals(gb, b->grant_len[g], expected);
+}
+
+/* MultiGrant index (certificate-relative) of every grant of certificate c:
+ * explicit CSR (cert_mg_off / mg_grant_off) or, without it, one MultiGrant per
+ * maximal run of equal signers.  Returns the MultiGrant count. */
+static uint32_t cert_multigrants(const mochi_batch* b, uint32_t c, uint32_t* mg_of /* [g_hi - g_lo] */) {
+  const uint32_t g_lo = b->cert_grant_off[c], g_hi = b->cert_grant_off[c + 1];
+  if (b->cert_mg_off && b->mg_grant_off) {
+    const uint32_t m_lo = b->cert_mg_off[c], m_hi = b->cert_mg_off[c + 1];
+    for (uint32_t m = m_lo; m < m_hi; m++)
+      for (uint32_t g = b->mg_grant_off[m]; g < b->mg_grant_off[m + 1]; g++) mg_of[g - g_lo] = m - m_lo;
+    return m_hi - m_lo;
+  }
+  uint32_t n = 0;
+  for (uint32_t g = g_lo; g < g_hi; g++) {
+    if (g == g_lo || b->signer[g] != b->signer[g - 1]) n++;
+    mg_of[g - g_lo] = n - 1;
+  }
+  return n;
+}
+
+/* StoreValueObjectContainer.getCurrentTimestampFromCurrentCertificate (:175-198)
+ * on the INCOMING certificate, as applyOperation calls it after setCurrentC(wc)
+ * (InMemoryDataStore.java:533-534):
+ *   for (multiGrant : currentC.grants.values())                 -- every MultiGrant
+ *     grant = multiGrant.grants.get(key)
+ *     Utils.assertNotNull(grant, ...)                          -- :186 -> IllegalStateException
+ *     if (timestamp == null) timestamp = grant.ts
+ *     else if (timestamp != grant.ts) throw IllegalStateException  -- :192-194
+ * Signatures play no part: the Java loop sees the certificate as received.
+ * Returns 1 and the timestamp, or 0 (throws). */
+static int incoming_cert_ts(const mochi_batch* b, uint32_t c, uint32_t slot, const int64_t* grant_ts,
+                            const uint32_t* mg_of, uint32_t n_mg, int64_t* ts_out) {
+  const uint32_t g_lo = b->cert_grant_off[c], g_hi = b->cert_grant_off[c + 1];
+  int have = 0;
+  int64_t ts = 0;
+  for (uint32_t m = 0; m < n_mg; m++) {
+    int found = 0;
+    for (uint32_t g = g_lo; g < g_hi; g++) {
+      if (mg_of[g - g_lo] != m || b->grant_key[g] != slot) continue;
+      found = 1;
+      if (!have) {
+        have = 1;
+        ts = grant_ts[g];
+      } else if (grant_ts[g] != ts) {
+        return 0;
+      }
+    }
+    if (!found) return 0;
+  }
+  if (!have) return 0; /* no MultiGrant at all: the Long is null and `long timestamp = ...` unboxes it (NPE) */
+  *ts_out = ts;
+  return 1;
+}
+
 int oracle_tally(const mochi_batch* b, const mochi_params* p, const uint8_t* grant_flags, const int64_t* grant_ts,
                  mochi_verdicts* out) {
   if (!b || !p || !grant_flags || !grant_ts || !out || !out->cert_accept_bits) return MOCHI_EINVAL;
   const uint32_t M = oracle_server_majority(p->replication_factor);
   memset(out->cert_accept_bits, 0, ((size_t)b->n_certs + 31) / 32 * 4);
+  uint32_t* mg_of = NULL;
+  size_t mg_cap = 0;
+  uint8_t* counted = NULL;
+  size_t cnt_cap = 0;
   for (uint32_t c = 0; c < b->n_certs; c++) {
     const uint32_t g_lo = b->cert_grant_off[c], g_hi = b->cert_grant_off[c + 1];
     const uint32_t o_lo = b->cert_op_off[c], o_hi = b->cert_op_off[c + 1];
-    const uint32_t n_ops = o_hi - o_lo;
+    const uint32_t n_ops = o_hi - o_lo, n_g = g_hi - g_lo;
+    const uint8_t* expected = b->expected_hash + (size_t)c * MOCHI_TXN_HASH_BYTES;
     uint8_t reason = MOCHI_ACCEPT, fail_op = 0xFF;
+    if (n_g > mg_cap) {
+      mg_cap = n_g * 2;
+      mg_of = (uint32_t*)realloc(mg_of, mg_cap * sizeof *mg_of);
+    }
+    if (n_g > cnt_cap) {
+      cnt_cap = n_g * 2;
+      counted = (uint8_t*)realloc(counted, cnt_cap);
+    }
+    const uint32_t n_mg = cert_multigrants(b, c, mg_of);
 
     /* Malformed grant bytes: the reference fails in the protobuf decoder
      * before any of the protocol code runs (MochiServerInitializer.java:30-34). */
     for (uint32_t g = g_lo; g < g_hi && reason == MOCHI_ACCEPT; g++)
       if (!(grant_flags[g] & MOCHI_GRANT_PARSED)) reason = MOCHI_REJECT_MALFORMED;
 
-    /* multiplicity of each key slot = number of txn ops naming that key */
-    uint32_t mult[MOCHI_MAX_OPS_PER_CERT];
-    int seen[MOCHI_MAX_OPS_PER_CERT];
-    int64_t ts0[MOCHI_MAX_OPS_PER_CERT];
-    uint32_t cnt[MOCHI_MAX_OPS_PER_CERT];
-    uint32_t first[MOCHI_MAX_OPS_PER_CERT];
+    /* multiplicity of each key slot = number of txn ops naming that key;
+     * first_op[s] = the first op naming slot s (its operand1 is the key) */
+    uint32_t mult[MOCHI_MAX_OPS_PER_CERT], first_op[MOCHI_MAX_OPS_PER_CERT];
     memset(mult, 0, sizeof mult);
-    memset(seen, 0, sizeof seen);
-    memset(cnt, 0, sizeof cnt);
-    for (uint32_t o = o_lo; o < o_hi; o++) mult[b->op_key[o]]++;
+    for (uint32_t o = o_hi; o-- > o_lo;) {
+      mult[b->op_key[o]]++;
+      first_op[b->op_key[o]] = o;
+    }
+
+    /* Which grants count.  Reference parity (quorum_mode 0): a grant counts iff
+     * its signature verified ("invalid signature => absent", the null skip at
+     * InMemoryDataStore.java:622-624) and an op names its key.  MOCHI_Q_BIND /
+     * MOCHI_Q_DISTINCT_SIGNERS exclude more grants the same way. */
+    for (uint32_t g = g_lo; g < g_hi; g++) {
+      const uint32_t s = b->grant_key[g];
+      int ok = (grant_flags[g] & MOCHI_GRANT_SIG_OK) && s < MOCHI_MAX_OPS_PER_CERT && mult[s] != 0;
+      if (ok && (p->quorum_mode & MOCHI_Q_BIND)) ok = grant_bound(b, g, first_op[s], expected);
+      if (ok && (p->quorum_mode & MOCHI_Q_DISTINCT_SIGNERS))
+        for (uint32_t q = g_lo; q < g && ok; q++)
+          if (counted[q - g_lo] && b->grant_key[q] == s && b->signer[q] == b->signer[g]) ok = 0;
+      counted[g - g_lo] = (uint8_t)ok;
+    }
 
     /* processMultiGrantsFromAllServers  InMemoryDataStore.java:613-640
      *   for (multiGrant : wc.grants.values())            -- wire order
      *     for (op : transaction.operations)              -- txn order
-     *       grant = multiGrant.grants.get(op.operand1)   -- (invalid signature => absent)
+     *       grant = multiGrant.grants.get(op.operand1)   -- (not counted => absent)
      *       if (grant == null) continue;                 -- :622-624
      *       if (coalesced.containsKey(key)) {
      *         if (coalesced[key].ts != grant.ts) throw UnsupportedOperationException  -- :626-628
@@ -500,62 +591,92 @@ int oracle_tally(const mochi_batch* b, const mochi_params* p, const uint8_t* gra
      * A grant for key slot s is appended once per op naming s (mult[s] times);
      * its own comparisons against ts0 all agree, so only the first sighting
      * per slot matters for ts0 and g0. */
-    for (uint32_t g = g_lo; g < g_hi && reason == MOCHI_ACCEPT; g++) {
-      if (!(grant_flags[g] & MOCHI_GRANT_SIG_OK)) continue;
+    int seen[MOCHI_MAX_OPS_PER_CERT];
+    int64_t ts0[MOCHI_MAX_OPS_PER_CERT];
+    uint32_t cnt[MOCHI_MAX_OPS_PER_CERT], first[MOCHI_MAX_OPS_PER_CERT];
+    memset(seen, 0, sizeof seen);
+    memset(cnt, 0, sizeof cnt);
+    int ts_bad = 0;
+    for (uint32_t g = g_lo; g < g_hi; g++) {
+      if (!counted[g - g_lo]) continue;
       const uint32_t s = b->grant_key[g];
-      if (s >= MOCHI_MAX_OPS_PER_CERT || mult[s] == 0) continue; /* never looked up */
       if (!seen[s]) {
         seen[s] = 1;
         ts0[s] = grant_ts[g];
         first[s] = g;
         cnt[s] = mult[s];
       } else {
-        if (ts0[s] != grant_ts[g]) {
-          reason = MOCHI_REJECT_TS_MISMATCH;
-          break;
-        }
+        if (ts0[s] != grant_ts[g]) ts_bad = 1;
         cnt[s] += mult[s];
       }
     }
+    if (reason == MOCHI_ACCEPT && ts_bad) reason = MOCHI_REJECT_TS_MISMATCH;
 
-    /* write2apply verdict part  InMemoryDataStore.java:576-611, ops in txn order */
+    /* write2apply  InMemoryDataStore.java:576-611, ops in txn order */
+    uint8_t decision[MOCHI_MAX_OPS_PER_CERT];
+    memset(decision, MOCHI_OPD_SKIPPED, sizeof decision);
+    int applied[MOCHI_MAX_OPS_PER_CERT]; /* slot s applied earlier in this txn: SVOC.currentC == wc */
+    memset(applied, 0, sizeof applied);
     for (uint32_t j = 0; j < n_ops && reason == MOCHI_ACCEPT; j++) {
       const uint32_t o = o_lo + j;
       const uint8_t fl = b->op_flags[o];
-      if (!(fl & MOCHI_OP_LOCAL)) continue; /* WRONG_SHARD result  :582-587 */
+      if (!(fl & MOCHI_OP_LOCAL)) { /* WRONG_SHARD result  :582-587 */
+        decision[j] = MOCHI_OPD_WRONG_SHARD;
+        continue;
+      }
       const uint32_t s = b->op_key[o];
-      if (!seen[s]) { /* coalescedTxnGrantMap.get(key) == null -> NPE  :588 */
-        reason = MOCHI_REJECT_NO_GRANT;
-        fail_op = (uint8_t)j;
-        break;
-      }
+      uint8_t why = MOCHI_ACCEPT;
+      if (!seen[s]) why = MOCHI_REJECT_NO_GRANT; /* coalescedTxnGrantMap.get(key) == null -> NPE  :588 */
       /* Utils.assertTrue(list.size() > getServerMajority())  :590 (client: >=) */
-      const int quorum_ok = p->strict_gt ? (cnt[s] > M) : (cnt[s] >= M);
-      if (!quorum_ok) {
-        reason = MOCHI_REJECT_BELOW_QUORUM;
-        fail_op = (uint8_t)j;
-        break;
-      }
+      else if (!(p->strict_gt ? (cnt[s] > M) : (cnt[s] >= M))) why = MOCHI_REJECT_BELOW_QUORUM;
       /* if (grantForObject.getTransactionHash().equals(txnHash)) ... else throw  :591,605-607 */
-      const uint32_t g0 = first[s];
-      if (!hash_equals(b->grant_bytes + b->grant_off[g0], b->grant_len[g0],
-                       b->expected_hash + (size_t)c * MOCHI_TXN_HASH_BYTES)) {
-        reason = MOCHI_REJECT_HASH_MISMATCH;
-        fail_op = (uint8_t)j;
-        break;
-      }
+      else if (!hash_equals(b->grant_bytes + b->grant_off[first[s]], b->grant_len[first[s]], expected))
+        why = MOCHI_REJECT_HASH_MISMATCH;
       /* storeValueContainer = getDataMap(key).get(key); op.getOperand1().equals(svoc.getKey()) -> NPE if null  :592-593 */
-      if (!(fl & MOCHI_OP_HAS_SVOC)) {
-        reason = MOCHI_REJECT_NO_SVOC;
+      else if (!(fl & MOCHI_OP_HAS_SVOC)) why = MOCHI_REJECT_NO_SVOC;
+      if (why == MOCHI_ACCEPT) {
+        /* Long objectTS = svoc.getCurrentTimestampFromCurrentCertificate()  :594 -- on the
+         * stored certificate: wc itself once an earlier op of this txn applied to this key */
+        const int has_cc = applied[s] || (fl & MOCHI_OP_HAS_CURRENT_C);
+        const int cc_bad = !applied[s] && (fl & MOCHI_OP_CURRENT_C_BAD);
+        const int64_t g0_ts = grant_ts[first[s]];
+        const int64_t obj_ts = applied[s] ? g0_ts : (b->op_object_ts ? b->op_object_ts[o] : 0);
+        if (cc_bad) {
+          why = MOCHI_REJECT_STORED_CERT;
+        } else {
+          /* if (objectTS != null && objectTS > g0.getTimestamp()) readOperation else applyOperation  :595-599;
+           * both first check the write lock and the action (:525-529 / :560-562, :551 / :572) */
+          const int read = has_cc && obj_ts > g0_ts;
+          int64_t t_in;
+          if (fl & MOCHI_OP_NOT_WRITE) why = MOCHI_REJECT_NOT_WRITE;
+          else if (read) decision[j] = MOCHI_OPD_READ;
+          /* applyOperation: setCurrentC(wc); getCurrentTimestampFromCurrentCertificate()  :533-534 */
+          else if (!incoming_cert_ts(b, c, s, grant_ts, mg_of, n_mg, &t_in)) why = MOCHI_REJECT_APPLY_STATE;
+          else {
+            decision[j] = MOCHI_OPD_APPLY;
+            applied[s] = 1; /* t_in == g0_ts: g0 is one of the grants the check compared */
+          }
+        }
+      }
+      if (why != MOCHI_ACCEPT) {
+        reason = why;
         fail_op = (uint8_t)j;
-        break;
+        decision[j] = MOCHI_OPD_FAILED;
       }
     }
 
     if (reason == MOCHI_ACCEPT) out->cert_accept_bits[c >> 5] |= 1u << (c & 31);
     if (out->cert_reason) out->cert_reason[c] = reason;
     if (out->cert_fail_op) out->cert_fail_op[c] = fail_op;
+    for (uint32_t j = 0; j < n_ops; j++) {
+      const uint32_t o = o_lo + j, s = b->op_key[o];
+      if (out->op_decision) out->op_decision[o] = decision[j];
+      if (out->op_g0) out->op_g0[o] = seen[s] ? first[s] - g_lo : 0xFFFFFFFFu;
+      if (out->op_ts) out->op_ts[o] = seen[s] ? grant_ts[first[s]] : 0;
+    }
   }
+  free(mg_of);
+  free(counted);
   return MOCHI_OK;
 }
 
@@ -952,9 +1073,40 @@ static void gout_push(gout_t* o, uint64_t off, uint32_t len, const uint8_t* sig,
   o->n++;
 }
 
-/* Decode message m (valid) into grants / ops; returns MOCHI_MSG_OK or MOCHI_MSG_FALLBACK. */
+/* Last value of varint field `field` (wire type 0) of [off, off+len); 0 when absent. */
+static uint64_t last_varint(const uint8_t* m, size_t off, size_t len, uint32_t field) {
+  fld_t f;
+  int rc;
+  uint64_t v = 0;
+  FOR_FIELDS(m, off, len, f, rc)
+    if (f.field == field && f.wt == 0) v = f.v;
+  return v;
+}
+
+typedef struct {
+  uint8_t key;     /* key slot: index of the first op with the same operand1 */
+  uint8_t notw;    /* MOCHI_OP_NOT_WRITE derived from the message            */
+  uint64_t k_off;  /* operand1 (absolute wire offset) and length            */
+  uint32_t k_len;
+} op_info_t;
+
+typedef struct {
+  uint32_t n, cap;
+  uint32_t* cnt; /* grants per MultiGrant */
+} mgout_t;
+
+static void mg_push(mgout_t* o, uint32_t n) {
+  if (o->n == o->cap) {
+    o->cap = o->cap ? o->cap * 2 : 1024;
+    o->cnt = (uint32_t*)realloc(o->cnt, o->cap * sizeof(uint32_t));
+  }
+  o->cnt[o->n++] = n;
+}
+
+/* Decode message m (valid) into grants / MultiGrants / ops; returns MOCHI_MSG_OK
+ * or MOCHI_MSG_FALLBACK. */
 static int decode_one(const uint8_t* m, size_t mlen, uint64_t base, const uint8_t* ids, const uint32_t* id_off,
-                      uint32_t n_ids, gout_t* go, uint8_t* op_key, uint32_t* n_ops) {
+                      uint32_t n_ids, gout_t* go, mgout_t* mo_out, op_info_t* ops, uint32_t* n_ops) {
   fld_t f;
   int rc;
   size_t wc_off = 0, wc_len = 0, tx_off = 0, tx_len = 0;
@@ -973,8 +1125,16 @@ static int decode_one(const uint8_t* m, size_t mlen, uint64_t base, const uint8_
     last_string(m, tx_off + f.off, f.len, 2, &op_o[no], &op_l[no]);
     uint32_t slot = no;
     for (uint32_t j = 0; j < no; j++)
-      if (same(m, op_o[j], op_l[j], op_o[no], op_l[no])) { slot = op_key[j]; break; }
-    op_key[no++] = (uint8_t)slot;
+      if (same(m, op_o[j], op_l[j], op_o[no], op_l[no])) { slot = ops[j].key; break; }
+    /* Operation.action (field 1, enum; proto3 open: any value but WRITE = 2 /
+     * DELETE = 1 fails applyOperation / readOperation, :529 / :562), and an empty
+     * operand1 is never write-locked (getObjectsToWriteLock, :339-358) */
+    const int32_t action = (int32_t)(uint32_t)last_varint(m, tx_off + f.off, f.len, 1);
+    ops[no].key = (uint8_t)slot;
+    ops[no].notw = (action != 1 && action != 2) || op_l[no] == 0 ? MOCHI_OP_NOT_WRITE : 0;
+    ops[no].k_off = base + op_o[no];
+    ops[no].k_len = (uint32_t)op_l[no];
+    no++;
   }
   *n_ops = no;
   /* certificate entries: WriteCertificate.grants (serverId -> MultiGrant) */
@@ -982,7 +1142,7 @@ static int decode_one(const uint8_t* m, size_t mlen, uint64_t base, const uint8_
   const size_t nce = list_entries(m, wc_off, wc_len, 1, &ce);
   int status = MOCHI_MSG_OK;
   uint32_t n_mg = 0;
-  const uint32_t g_start = go->n;
+  const uint32_t g_start = go->n, mg_start = mo_out->n;
   for (size_t i = 0; i < nce && status == MOCHI_MSG_OK; i++)
     if (ce[i].nval > 1) status = MOCHI_MSG_FALLBACK;
   for (size_t i = 0; i < nce && status == MOCHI_MSG_OK; i++) {
@@ -1013,14 +1173,18 @@ static int decode_one(const uint8_t* m, size_t mlen, uint64_t base, const uint8_
           sig = se[q].vlen == MOCHI_RSA_BYTES ? m + se[q].voff : NULL;
       uint8_t key = 0xFF;
       for (uint32_t j = 0; j < no; j++)
-        if (same(m, op_o[j], op_l[j], ge[a].koff, ge[a].klen)) { key = op_key[j]; break; }
+        if (same(m, op_o[j], op_l[j], ge[a].koff, ge[a].klen)) { key = ops[j].key; break; }
       gout_push(go, base + ge[t].voff, (uint32_t)ge[t].vlen, sig, signer, key);
     }
+    if (status == MOCHI_MSG_OK) mg_push(mo_out, n_g);
     free(ge);
     free(se);
   }
   free(ce);
-  if (status != MOCHI_MSG_OK) go->n = g_start; /* drop partial output */
+  if (status != MOCHI_MSG_OK) { /* drop partial output */
+    go->n = g_start;
+    mo_out->n = mg_start;
+  }
   return status;
 }
 
@@ -1031,43 +1195,64 @@ int oracle_w2_decode(const mochi_write2_batch* w, const uint8_t* ids, const uint
   const uint32_t M = w->n_msgs;
   gout_t go;
   memset(&go, 0, sizeof go);
+  mgout_t mg;
+  memset(&mg, 0, sizeof mg);
   uint32_t* cg = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
   uint32_t* co = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
+  uint32_t* cm = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
   uint8_t* st = (uint8_t*)calloc(M ? M : 1, 1);
   size_t ocap = 1024, on = 0;
   uint8_t* opk = (uint8_t*)malloc(ocap);
   uint8_t* opf = (uint8_t*)malloc(ocap);
+  int64_t* opt = (int64_t*)malloc(ocap * sizeof(int64_t));
+  uint64_t* oko = (uint64_t*)malloc(ocap * sizeof(uint64_t));
+  uint32_t* okl = (uint32_t*)malloc(ocap * sizeof(uint32_t));
   for (uint32_t i = 0; i < M; i++) {
     const uint8_t* m = w->wire + w->msg_off[i];
     const size_t ml = w->msg_len[i];
-    uint8_t keys[MOCHI_MAX_OPS_PER_CERT];
+    op_info_t ops[MOCHI_MAX_OPS_PER_CERT];
     uint32_t no = 0;
-    int s = valid_write2(m, ml) ? decode_one(m, ml, w->msg_off[i], ids, id_off, n_ids, &go, keys, &no)
+    const uint32_t mg0 = mg.n;
+    int s = valid_write2(m, ml) ? decode_one(m, ml, w->msg_off[i], ids, id_off, n_ids, &go, &mg, ops, &no)
                                 : MOCHI_MSG_MALFORMED;
     if (s == MOCHI_MSG_OK && w->op_flags_off && w->op_flags_off[i + 1] - w->op_flags_off[i] != no)
       s = MOCHI_MSG_OPS_MISMATCH;
     if (s != MOCHI_MSG_OK) {
       no = 0;
       go.n = cg[i];
+      mg.n = mg0;
     }
     st[i] = (uint8_t)s;
     if (on + no > ocap) {
       while (on + no > ocap) ocap *= 2;
       opk = (uint8_t*)realloc(opk, ocap);
       opf = (uint8_t*)realloc(opf, ocap);
+      opt = (int64_t*)realloc(opt, ocap * sizeof(int64_t));
+      oko = (uint64_t*)realloc(oko, ocap * sizeof(uint64_t));
+      okl = (uint32_t*)realloc(okl, ocap * sizeof(uint32_t));
     }
     for (uint32_t j = 0; j < no; j++) {
-      opk[on + j] = keys[j];
-      opf[on + j] = w->op_flags_off ? w->op_flags[w->op_flags_off[i] + j] : (MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
+      const size_t src = w->op_flags_off ? w->op_flags_off[i] + j : 0;
+      opk[on + j] = ops[j].key;
+      opf[on + j] = (uint8_t)((w->op_flags_off ? w->op_flags[src] : (MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC)) | ops[j].notw);
+      opt[on + j] = w->op_flags_off && w->op_object_ts ? w->op_object_ts[src] : 0;
+      oko[on + j] = ops[j].k_off;
+      okl[on + j] = ops[j].k_len;
     }
     on += no;
     cg[i + 1] = go.n;
     co[i + 1] = (uint32_t)on;
+    cm[i + 1] = mg.n;
   }
+  uint32_t* mgo = (uint32_t*)malloc(((size_t)mg.n + 1) * sizeof(uint32_t));
+  mgo[0] = 0;
+  for (uint32_t j = 0; j < mg.n; j++) mgo[j + 1] = mgo[j] + mg.cnt[j];
+  free(mg.cnt);
   mochi_batch* b = &out->batch;
   b->n_grants = go.n;
   b->n_certs = M;
   b->n_ops = (uint32_t)on;
+  b->n_mgs = mg.n;
   b->grant_bytes_len = w->wire_len;
   b->grant_bytes = w->wire;
   b->grant_off = go.off;
@@ -1080,6 +1265,11 @@ int oracle_w2_decode(const mochi_write2_batch* w, const uint8_t* ids, const uint
   b->op_key = opk;
   b->op_flags = opf;
   b->expected_hash = w->expected_hash;
+  b->cert_mg_off = cm;
+  b->mg_grant_off = mgo;
+  b->op_object_ts = opt;
+  b->op_key_off = oko;
+  b->op_key_len = okl;
   out->msg_status = st;
   return MOCHI_OK;
 }
@@ -1095,6 +1285,11 @@ void oracle_w2_free(oracle_w2_decoded* d) {
   free((void*)d->batch.cert_op_off);
   free((void*)d->batch.op_key);
   free((void*)d->batch.op_flags);
+  free((void*)d->batch.cert_mg_off);
+  free((void*)d->batch.mg_grant_off);
+  free((void*)d->batch.op_object_ts);
+  free((void*)d->batch.op_key_off);
+  free((void*)d->batch.op_key_len);
   free(d->msg_status);
   memset(d, 0, sizeof *d);
 }
@@ -1105,19 +1300,41 @@ int oracle_verify_write2(const uint8_t* moduli_be, uint32_t n_keys, const uint8_
   oracle_w2_decoded d;
   int rc = oracle_w2_decode(w, ids, id_off, n_keys, &d);
   if (rc) return rc;
+  const uint32_t O = d.batch.n_ops;
+  const int per_op = out->op_decision || out->op_g0 || out->op_ts;
+  if (per_op && !w->op_flags_off) {
+    oracle_w2_free(&d);
+    return MOCHI_EINVAL;
+  }
   mochi_verdicts v = *out;
   v.grant_valid_bits = NULL;
   v.grant_flags = NULL;
   v.grant_ts = NULL;
+  /* per-op results in decoded order, scattered to the op_flags_off layout below */
+  v.op_decision = (uint8_t*)malloc(O ? O : 1);
+  v.op_g0 = (uint32_t*)malloc(sizeof(uint32_t) * (O ? O : 1));
+  v.op_ts = (int64_t*)malloc(sizeof(int64_t) * (O ? O : 1));
   rc = oracle_verify_batch(moduli_be, n_keys, &d.batch, p, &v, n_threads);
   for (uint32_t i = 0; rc == MOCHI_OK && i < w->n_msgs; i++) {
     const uint8_t s = d.msg_status[i];
     if (msg_status) msg_status[i] = s;
+    if (per_op) {
+      const uint32_t lo = w->op_flags_off[i], hi = w->op_flags_off[i + 1], dlo = d.batch.cert_op_off[i];
+      for (uint32_t o = lo; o < hi; o++) {
+        const int ok = s == MOCHI_MSG_OK;
+        if (out->op_decision) out->op_decision[o] = ok ? v.op_decision[dlo + o - lo] : MOCHI_OPD_SKIPPED;
+        if (out->op_g0) out->op_g0[o] = ok ? v.op_g0[dlo + o - lo] : 0xFFFFFFFFu;
+        if (out->op_ts) out->op_ts[o] = ok ? v.op_ts[dlo + o - lo] : 0;
+      }
+    }
     if (s == MOCHI_MSG_OK) continue;
     out->cert_accept_bits[i >> 5] &= ~(1u << (i & 31));
     if (out->cert_reason) out->cert_reason[i] = s == MOCHI_MSG_MALFORMED ? MOCHI_REJECT_MALFORMED : MOCHI_UNDECIDED;
     if (out->cert_fail_op) out->cert_fail_op[i] = 0xFF;
   }
+  free(v.op_decision);
+  free(v.op_g0);
+  free(v.op_ts);
   oracle_w2_free(&d);
   return rc;
 }

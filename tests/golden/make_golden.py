@@ -23,6 +23,7 @@ from __future__ import annotations
 import hashlib
 import json
 import os
+import sys
 import subprocess
 import tempfile
 
@@ -206,76 +207,142 @@ def rsa_vectors():
 def cert_cases():
     """Hand-constructed certificates for every verdict branch.
 
-    Grant spec: [server, key_slot, ts, hash ('good'|'evil'|'short'), sig ('ok'|'bad'), bytes ('ok'|'malformed')],
-    listed in certificate wire order (MultiGrant by MultiGrant).  Ops: [key_slot, flags] in txn order
-    (flags: 1 = local shard, 2 = SVOC exists).  Expected reason codes are read off the Java source.
+    Grant spec: [server, key_slot, ts, hash ('good'|'evil'|'short'), sig ('ok'|'bad'), bytes ('ok'|'malformed'),
+    optional extras {"mg": MultiGrant index, "oid": key slot written as Grant.objectId}], listed in certificate
+    wire order (MultiGrant by MultiGrant).  Without "mg" every maximal run of one server's grants is one
+    MultiGrant; a case may set "n_mgs" to add empty MultiGrants at the end.  Ops: [key_slot, flags, object_ts?]
+    in txn order (flags: 1 = local shard, 2 = SVOC exists, 4 = SVOC holds a certificate whose timestamp is
+    object_ts, 8 = that stored certificate throws, 16 = not a WRITE/DELETE).  quorum_mode: 0 = reference parity,
+    1 = distinct signers, 2 = bind objectId / transactionHash.  Expected reason codes, failing ops, per-op
+    decisions (0 skipped, 1 apply, 2 read, 3 wrong shard, 4 failed) and g0 (certificate-relative grant index,
+    -1 none) are read off the Java source (InMemoryDataStore.java:521-640, StoreValueObjectContainer.java:175-198).
     """
     G, E = "good", "evil"
     ok4 = [[r, 0, 1000, G, "ok", "ok"] for r in range(4)]
     c = []
-    c.append(dict(name="accept_4of4_server", R=4, strict=1, grants=ok4, ops=[[0, 3]], reason=0, fail_op=255,
-                  why="4 grants, list.size()=4 > M=3 (InMemoryDataStore.java:590); g0 hash equal (:591)"))
-    c.append(dict(name="below_quorum_3of4_server", R=4, strict=1, grants=ok4[:3], ops=[[0, 3]], reason=3, fail_op=0,
-                  why="list.size()=3 > M=3 is false -> Utils.assertTrue throws IllegalStateException (:590)"))
-    c.append(dict(name="client_predicate_3of4_accepts", R=4, strict=0, grants=ok4[:3], ops=[[0, 3]], reason=0,
-                  fail_op=255, why="client predicate count >= M (MochiDBClient.java:172,379): 3 >= 3"))
-    c.append(dict(name="invalid_sig_counts_as_absent", R=4, strict=1,
-                  grants=[ok4[0], ok4[1], [2, 0, 1000, G, "bad", "ok"], ok4[3]], ops=[[0, 3]], reason=3, fail_op=0,
-                  why="bad signature => grant treated as absent (:622-624 null skip) -> 3 grants -> below quorum"))
-    c.append(dict(name="ts_mismatch", R=4, strict=1,
-                  grants=[ok4[0], ok4[1], [2, 0, 1001, G, "ok", "ok"], ok4[3]], ops=[[0, 3]], reason=1, fail_op=255,
-                  why="valid grant with ts != first ts -> UnsupportedOperationException (:626-628)"))
-    c.append(dict(name="ts_mismatch_on_invalid_sig_ignored", R=4, strict=0,
-                  grants=[ok4[0], ok4[1], [2, 0, 1001, G, "bad", "ok"], ok4[3]], ops=[[0, 3]], reason=0, fail_op=255,
-                  why="the skewed grant has a bad signature, so it is absent; 3 >= 3 under the client predicate"))
-    c.append(dict(name="g0_hash_mismatch", R=4, strict=1,
-                  grants=[[0, 0, 1000, E, "ok", "ok"]] + ok4[1:], ops=[[0, 3]], reason=4, fail_op=0,
-                  why="g0.transactionHash != txnHash -> UnsupportedOperationException (:591,605-607)"))
-    c.append(dict(name="g1_hash_mismatch_accepted", R=4, strict=1,
-                  grants=[ok4[0], [1, 0, 1000, E, "ok", "ok"]] + ok4[2:], ops=[[0, 3]], reason=0, fail_op=255,
-                  why="only g0 = list.get(0) is compared (:588,591)"))
-    c.append(dict(name="g0_invalid_then_g1_evil", R=4, strict=0,
-                  grants=[[0, 0, 1000, G, "bad", "ok"], [1, 0, 1000, E, "ok", "ok"]] + ok4[2:], ops=[[0, 3]],
-                  reason=4, fail_op=0, why="g0 absent (bad sig) so the first VALID grant (evil hash) becomes list.get(0)"))
-    c.append(dict(name="hash_wrong_length", R=4, strict=1,
-                  grants=[[0, 0, 1000, "short", "ok", "ok"]] + ok4[1:], ops=[[0, 3]], reason=4, fail_op=0,
-                  why="String.equals fails on a 127-char hash"))
-    c.append(dict(name="no_grant_for_key", R=4, strict=1, grants=ok4, ops=[[0, 3], [1, 3]], reason=2, fail_op=1,
-                  why="op 1's key has no grant: coalescedTxnGrantMap.get(key) == null -> NPE (:588)"))
-    c.append(dict(name="wrong_shard_op_skipped", R=4, strict=1, grants=ok4, ops=[[0, 3], [1, 2]], reason=0,
-                  fail_op=255, why="op 1 not on this shard -> WRONG_SHARD result, no checks (:582-587)"))
-    c.append(dict(name="no_svoc", R=4, strict=1, grants=ok4, ops=[[0, 1]], reason=5, fail_op=0,
-                  why="storeValueContainer == null -> op.getOperand1().equals(svoc.getKey()) NPE (:592-593)"))
-    c.append(dict(name="duplicate_op_doubles_count", R=4, strict=1, grants=ok4[:2], ops=[[0, 3], [0, 3]], reason=0,
-                  fail_op=255, why="each op appends the grant again (:620-630): 2 grants x 2 ops = 4 > 3"))
-    c.append(dict(name="two_keys_accept", R=4, strict=1,
-                  grants=[[r, s, 1000 + 7 * s, G, "ok", "ok"] for r in range(4) for s in range(2)],
-                  ops=[[0, 3], [1, 3]], reason=0, fail_op=255, why="per-key lists, ts uniform per key only"))
-    c.append(dict(name="two_keys_second_below_quorum", R=4, strict=1,
-                  grants=[[r, s, 1000, G, "ok" if (r, s) != (3, 1) else "bad", "ok"] for r in range(4) for s in range(2)],
-                  ops=[[0, 3], [1, 3]], reason=3, fail_op=1, why="key 1 has 3 valid grants; op 0 passes first"))
-    c.append(dict(name="ts_mismatch_beats_quorum", R=4, strict=1,
-                  grants=[[0, 0, 1000, G, "ok", "ok"], [1, 0, 1002, G, "ok", "ok"]], ops=[[0, 3]], reason=1,
-                  fail_op=255, why="processMultiGrantsFromAllServers runs before write2apply (:646 vs :653)"))
-    c.append(dict(name="malformed_grant_rejects", R=4, strict=0,
-                  grants=ok4[:3] + [[3, 0, 1000, G, "ok", "malformed"]], ops=[[0, 3]], reason=6, fail_op=255,
-                  why="unparseable Grant bytes: protobuf decode fails before the handler runs"))
-    c.append(dict(name="grant_for_unnamed_key_ignored", R=4, strict=1, grants=ok4 + [[0, 5, 77, E, "ok", "ok"]],
-                  ops=[[0, 3]], reason=0, fail_op=255, why="grants whose key no op names are never looked up (:621)"))
-    c.append(dict(name="r7_server_6of7_accepts", R=7, strict=1, grants=[[r, 0, 5000, G, "ok", "ok"] for r in range(6)],
-                  ops=[[0, 3]], reason=0, fail_op=255, why="R=7: M=2*(7/3)+1=5 (ClusterConfiguration.java:264-267); 6 > 5"))
-    c.append(dict(name="r7_server_5of7_rejects", R=7, strict=1, grants=[[r, 0, 5000, G, "ok", "ok"] for r in range(5)],
-                  ops=[[0, 3]], reason=3, fail_op=0, why="R=7: 5 > 5 is false under the server predicate"))
-    c.append(dict(name="r7_client_5of7_accepts", R=7, strict=0, grants=[[r, 0, 5000, G, "ok", "ok"] for r in range(5)],
-                  ops=[[0, 3]], reason=0, fail_op=255, why="client predicate 5 >= 5 (the BASELINE '5-of-7 tally')"))
-    c.append(dict(name="empty_certificate_no_ops", R=4, strict=1, grants=[], ops=[], reason=0, fail_op=255,
-                  why="no ops -> write2apply loop empty -> accepted"))
-    c.append(dict(name="empty_certificate_with_op", R=4, strict=1, grants=[], ops=[[0, 3]], reason=2, fail_op=0,
-                  why="no grants at all -> NPE on the first local op (:588)"))
+
+    def add(name, R, strict, grants, ops, reason, fail_op, decisions, g0, why, **kw):
+        c.append(dict(name=name, R=R, strict=strict, grants=grants, ops=ops, reason=reason, fail_op=fail_op,
+                      decisions=decisions, g0=g0, why=why, quorum_mode=kw.pop("quorum_mode", 0), **kw))
+
+    add("accept_4of4_server", 4, 1, ok4, [[0, 3]], 0, 255, [1], [0],
+        "4 grants, list.size()=4 > M=3 (InMemoryDataStore.java:590); g0 hash equal (:591); no stored "
+        "certificate -> applyOperation (:597); every MultiGrant holds the key at ts 1000 (SVOC :186-194)")
+    add("below_quorum_3of4_server", 4, 1, ok4[:3], [[0, 3]], 3, 0, [4], [0],
+        "list.size()=3 > M=3 is false -> Utils.assertTrue throws IllegalStateException (:590)")
+    add("client_predicate_3of4_accepts", 4, 0, ok4[:3], [[0, 3]], 0, 255, [1], [0],
+        "client predicate count >= M (MochiDBClient.java:172,379): 3 >= 3")
+    add("invalid_sig_counts_as_absent", 4, 1, [ok4[0], ok4[1], [2, 0, 1000, G, "bad", "ok"], ok4[3]], [[0, 3]], 3, 0,
+        [4], [0], "bad signature => grant treated as absent (:622-624 null skip) -> 3 grants -> below quorum")
+    add("ts_mismatch", 4, 1, [ok4[0], ok4[1], [2, 0, 1001, G, "ok", "ok"], ok4[3]], [[0, 3]], 1, 255, [0], [0],
+        "valid grant with ts != first ts -> UnsupportedOperationException (:626-628)")
+    add("ts_skew_on_invalid_sig_fails_apply", 4, 0, [ok4[0], ok4[1], [2, 0, 1001, G, "bad", "ok"], ok4[3]], [[0, 3]],
+        8, 0, [4], [0],
+        "the skewed grant has a bad signature, so the tally skips it (3 >= 3 passes), but applyOperation stores the "
+        "certificate as received and getCurrentTimestampFromCurrentCertificate compares every MultiGrant: 1001 != "
+        "1000 -> IllegalStateException (:533-534, StoreValueObjectContainer.java:192-194)")
+    add("ts_skew_on_invalid_sig_read_branch_accepts", 4, 0,
+        [ok4[0], ok4[1], [2, 0, 1001, G, "bad", "ok"], ok4[3]], [[0, 7, 5000]], 0, 255, [2], [0],
+        "same certificate, but the SVOC's stored certificate has ts 5000 > g0.ts 1000 -> readOperation (:595-596), "
+        "which never looks at the incoming certificate")
+    add("g0_hash_mismatch", 4, 1, [[0, 0, 1000, E, "ok", "ok"]] + ok4[1:], [[0, 3]], 4, 0, [4], [0],
+        "g0.transactionHash != txnHash -> UnsupportedOperationException (:591,605-607)")
+    add("g1_hash_mismatch_accepted", 4, 1, [ok4[0], [1, 0, 1000, E, "ok", "ok"]] + ok4[2:], [[0, 3]], 0, 255, [1],
+        [0], "only g0 = list.get(0) is compared (:588,591)")
+    add("g0_invalid_then_g1_evil", 4, 0, [[0, 0, 1000, G, "bad", "ok"], [1, 0, 1000, E, "ok", "ok"]] + ok4[2:],
+        [[0, 3]], 4, 0, [4], [1], "g0 absent (bad sig) so the first VALID grant (evil hash) becomes list.get(0)")
+    add("hash_wrong_length", 4, 1, [[0, 0, 1000, "short", "ok", "ok"]] + ok4[1:], [[0, 3]], 4, 0, [4], [0],
+        "String.equals fails on a 127-char hash")
+    add("no_grant_for_key", 4, 1, ok4, [[0, 3], [1, 3]], 2, 1, [1, 4], [0, -1],
+        "op 1's key has no grant: coalescedTxnGrantMap.get(key) == null -> NPE (:588); op 0 was already applied "
+        "(the loop is not atomic)")
+    add("wrong_shard_op_skipped", 4, 1, ok4, [[0, 3], [1, 2]], 0, 255, [1, 3], [0, -1],
+        "op 1 not on this shard -> WRONG_SHARD result, no checks (:582-587)")
+    add("no_svoc", 4, 1, ok4, [[0, 1]], 5, 0, [4], [0],
+        "storeValueContainer == null -> op.getOperand1().equals(svoc.getKey()) NPE (:592-593)")
+    add("duplicate_op_doubles_count", 4, 1, ok4[:2], [[0, 3], [0, 3]], 0, 255, [1, 1], [0, 0],
+        "each op appends the grant again (:620-630): 2 grants x 2 ops = 4 > 3; op 1 sees currentC = wc (ts 1000, "
+        "not > g0.ts) -> applies again")
+    add("two_keys_accept", 4, 1, [[r, s, 1000 + 7 * s, G, "ok", "ok"] for r in range(4) for s in range(2)],
+        [[0, 3], [1, 3]], 0, 255, [1, 1], [0, 1], "per-key lists, ts uniform per key only")
+    add("two_keys_second_below_quorum", 4, 1,
+        [[r, s, 1000, G, "ok" if (r, s) != (3, 1) else "bad", "ok"] for r in range(4) for s in range(2)],
+        [[0, 3], [1, 3]], 3, 1, [1, 4], [0, 1], "key 1 has 3 valid grants; op 0 passes (and applies) first")
+    add("ts_mismatch_beats_quorum", 4, 1, [[0, 0, 1000, G, "ok", "ok"], [1, 0, 1002, G, "ok", "ok"]], [[0, 3]], 1,
+        255, [0], [0], "processMultiGrantsFromAllServers runs before write2apply (:646 vs :653)")
+    add("malformed_grant_rejects", 4, 0, ok4[:3] + [[3, 0, 1000, G, "ok", "malformed"]], [[0, 3]], 6, 255, [0], [0],
+        "unparseable Grant bytes: protobuf decode fails before the handler runs")
+    add("grant_for_unnamed_key_ignored", 4, 1, [ok4[0], [0, 5, 77, E, "ok", "ok"]] + ok4[1:], [[0, 3]], 0, 255, [1],
+        [0], "grants whose key no op names are never looked up (:621, SVOC :185 looks up only the op's key)")
+    add("r7_server_6of7_accepts", 7, 1, [[r, 0, 5000, G, "ok", "ok"] for r in range(6)], [[0, 3]], 0, 255, [1], [0],
+        "R=7: M=2*(7/3)+1=5 (ClusterConfiguration.java:264-267); 6 > 5")
+    add("r7_server_5of7_rejects", 7, 1, [[r, 0, 5000, G, "ok", "ok"] for r in range(5)], [[0, 3]], 3, 0, [4], [0],
+        "R=7: 5 > 5 is false under the server predicate")
+    add("r7_client_5of7_accepts", 7, 0, [[r, 0, 5000, G, "ok", "ok"] for r in range(5)], [[0, 3]], 0, 255, [1], [0],
+        "client predicate 5 >= 5 (the BASELINE '5-of-7 tally')")
+    add("empty_certificate_no_ops", 4, 1, [], [], 0, 255, [], [], "no ops -> write2apply loop empty -> accepted")
+    add("empty_certificate_with_op", 4, 1, [], [[0, 3]], 2, 0, [4], [-1],
+        "no grants at all -> NPE on the first local op (:588)")
+    # --- the read/apply step (InMemoryDataStore.java:594-599, :521-574) ---
+    add("mg_without_key_fails_apply", 4, 1,
+        [g + [{"mg": i}] for i, g in enumerate(ok4)] + [[0, 1, 1000, G, "ok", "ok", {"mg": 4}]], [[0, 3]], 8, 0, [4], [0],
+        "a fifth MultiGrant carries only a grant for a key no op names: the tally never looks it up, but "
+        "getCurrentTimestampFromCurrentCertificate does: grants.get(key) == null -> Utils.assertNotNull throws "
+        "IllegalStateException (StoreValueObjectContainer.java:186)")
+    add("empty_mg_fails_apply", 4, 1, [g + [{"mg": i}] for i, g in enumerate(ok4)],
+        [[0, 3]], 8, 0, [4], [0], "an empty fifth MultiGrant: grants.get(key) == null (:186)", n_mgs=5)
+    add("read_branch_stored_ts_newer", 4, 1, ok4, [[0, 7, 2000]], 0, 255, [2], [0],
+        "objectTS 2000 > g0.ts 1000 -> readOperation (:595-596)")
+    add("apply_branch_stored_ts_equal", 4, 1, ok4, [[0, 7, 1000]], 0, 255, [1], [0],
+        "objectTS 1000 > 1000 is false -> applyOperation (:597)")
+    add("apply_branch_stored_ts_older", 4, 1, ok4, [[0, 7, 999]], 0, 255, [1], [0],
+        "objectTS 999 < g0.ts -> applyOperation")
+    add("stored_cert_throws", 4, 1, ok4, [[0, 15, 0]], 9, 0, [4], [0],
+        "the SVOC's stored certificate throws in getCurrentTimestampFromCurrentCertificate (:594)")
+    add("not_write_op_apply_branch", 4, 1, ok4, [[0, 19]], 10, 0, [4], [0],
+        "a READ op in a Write2 transaction: no write lock (:339-358) -> applyOperation throws (:525-526)")
+    add("not_write_op_read_branch", 4, 1, ok4, [[0, 23, 2000]], 10, 0, [4], [0],
+        "readOperation checks the lock / action too (:560-562, :572)")
+    add("duplicate_op_read_then_read", 4, 1, ok4[:2], [[0, 7, 2000], [0, 7, 2000]], 0, 255, [2, 2], [0, 0],
+        "readOperation leaves currentC alone, so the second op reads too")
+    add("duplicate_op_apply_then_apply", 4, 1, ok4[:2], [[0, 7, 500], [0, 7, 5000]], 0, 255, [1, 1], [0, 0],
+        "op 0 applies (500 < 1000) and stores wc; op 1's objectTS is then wc's 1000, not the stale 5000 -> applies")
+    add("stored_cert_bad_replaced_by_apply", 4, 1, ok4, [[0, 3], [0, 11, 0]], 0, 255, [1, 1], [0, 0],
+        "op 0 applies and replaces the bad stored certificate; op 1 sees wc")
+    add("two_keys_second_fails_apply", 4, 0,
+        [[r, s, 1000, G, "ok", "ok"] for r in range(4) for s in range(2) if (r, s) != (3, 1)],
+        [[0, 3], [1, 3]], 8, 1, [1, 4], [0, 1],
+        "key 1: 3 grants >= 3 (client predicate) but the fourth MultiGrant lacks it -> op 0 applied, op 1 throws "
+        "in getCurrentTimestampFromCurrentCertificate (:186)")
+    # --- quorum modes (the new signature layer as a Byzantine quorum; parity = mode 0) ---
+    same_signer = [[0, 0, 1000, G, "ok", "ok", {"mg": i}] for i in range(4)]
+    add("one_signer_four_map_keys_parity", 4, 1, same_signer, [[0, 3]], 0, 255, [1], [0],
+        "parity: list.size() counts entries (:590), so 4 copies of server 0's MultiGrant under 4 certificate map "
+        "keys reach 4 > 3")
+    add("one_signer_four_map_keys_distinct", 4, 1, same_signer, [[0, 3]], 3, 0, [4], [0],
+        "MOCHI_Q_DISTINCT_SIGNERS: server 0 counts once -> 1 > 3 fails", quorum_mode=1)
+    add("distinct_signers_honest_accepts", 4, 1, ok4, [[0, 3]], 0, 255, [1], [0],
+        "four different signers: unaffected by MOCHI_Q_DISTINCT_SIGNERS", quorum_mode=1)
+    foreign = ok4[:3] + [[3, 0, 1000, G, "ok", "ok", {"oid": 7}]]
+    add("foreign_object_grant_parity", 4, 1, foreign, [[0, 3]], 0, 255, [1], [0],
+        "parity: server 3's grant for another object (objectId CASE_KEY_7) filed under key 0 still counts")
+    add("foreign_object_grant_bind", 4, 1, foreign, [[0, 3]], 3, 0, [4], [0],
+        "MOCHI_Q_BIND: objectId != map key -> not counted -> 3 > 3 fails", quorum_mode=2)
+    add("foreign_txn_grant_bind", 4, 1, ok4[:3] + [[3, 0, 1000, E, "ok", "ok"]], [[0, 3]], 3, 0, [4], [0],
+        "MOCHI_Q_BIND: transactionHash != expected -> not counted (parity only checks g0)", quorum_mode=2)
+    add("bind_honest_accepts", 4, 1, ok4, [[0, 3]], 0, 255, [1], [0], "honest grants are bound", quorum_mode=2)
+    add("bind_and_distinct", 4, 0, same_signer[:2] + [[1, 0, 1000, G, "ok", "ok", {"mg": 2}],
+                                                      [2, 0, 1000, E, "ok", "ok", {"mg": 3}]], [[0, 3]], 3, 0, [4],
+        [0], "mode 3: server 0 once, server 1 once, server 2's grant is for another txn -> 2 >= 3 fails",
+        quorum_mode=3)
     return c
 
 
 def main():
+    if sys.argv[1:] == ["cert_cases"]:  # regenerate only the hand-constructed verdict cases
+        with open(os.path.join(HERE, "cert_cases.json"), "w") as f:
+            json.dump(cert_cases(), f, indent=1)
+        return
     with open(os.path.join(HERE, "sha256_vectors.json"), "w") as f:
         json.dump(sha256_vectors(), f, indent=1)
     gv, pv = grant_vectors()

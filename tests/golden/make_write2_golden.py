@@ -167,6 +167,12 @@ def vectors():
     add("grant_entry_empty_value", w2([(SID[0], mg(SID[0], [(A, b""), (B, gB[0])], [(A, sig(0)), (B, sig(1))])),
                                        base_mgs[1], base_mgs[2]], base_ops), 0, order3)
     add("action_unknown_enum", w2(base_mgs, [W.encode_operation(9, A, "v"), op(B)]), 0, order3)
+    # Operation.action / operand1 drive MOCHI_OP_NOT_WRITE (the read/apply step throws unless WRITE / DELETE
+    # with a non-empty, hence write-locked, operand1: InMemoryDataStore.java:339-358, :529, :562)
+    add("action_read_and_delete", w2(base_mgs, [W.encode_operation(0, A), W.encode_operation(1, B)]), 0, order3)
+    add("action_given_twice_last_wins", w2(base_mgs, [b"\x08\x00" + op(A), op(B) + b"\x08\x00"]), 0, order3)
+    add("operand1_empty", w2(base_mgs, [op(A), W.encode_operation(2, "", "v")]), 0,
+        {"certs": [SID[0], SID[1], SID[2]], "grants": [[A, B]] * 3, "ops": [A, ""]})
     add("utf8_multibyte_keys", w2([(SID[0], mg(SID[0], [("clé-ü", g("clé-ü", 5))], [("clé-ü", sig(3))]))],
                                   [op("clé-ü")]), 0, {"certs": [SID[0]], "grants": [["clé-ü"]], "ops": ["clé-ü"]})
     # fast-path exits (legal protobuf, host fallback)
@@ -239,7 +245,8 @@ def main():
                     "grants": {gk: gv.SerializeToString(deterministic=True).hex() for gk, gv in mgv.grants.items()},
                     "sigs": {sk: sv.hex() for sk, sv in mgv.grantSignatures.items()},
                 }
-            v["py_content"] = {"certs": content, "ops": [o.operand1 for o in m.transaction.operations]}
+            v["py_content"] = {"certs": content, "ops": [o.operand1 for o in m.transaction.operations],
+                               "actions": [int(o.action) for o in m.transaction.operations]}
         except Exception as ex:
             v["py_ok"] = False
             v["py_error"] = type(ex).__name__

@@ -121,14 +121,15 @@ def _moduli_buf(moduli):
     return m
 
 
-def verify_batch(moduli, batch, replication_factor: int, strict_gt: bool = True, n_threads: int = 8):
+def verify_batch(moduli, batch, replication_factor: int, strict_gt: bool = True, n_threads: int = 8,
+                 quorum_mode: int = 0):
     """Oracle verdicts for a mochi_hip.Batch (host memory)."""
     import mochi_hip as mh
 
     b = batch.normalized()
-    out = mh.Verdicts.alloc(b.n_grants, b.n_certs)
+    out = mh.Verdicts.alloc(b.n_grants, b.n_certs, b.n_ops)
     bc, vc = b.to_c(), out.to_c()
-    p = mh.Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+    p = mh.params(replication_factor, strict_gt, quorum_mode)
     m = _moduli_buf(moduli)
     rc = lib().oracle_verify_batch(m.ctypes.data, len(moduli), ctypes.byref(bc), ctypes.byref(p), ctypes.byref(vc),
                                    n_threads)
@@ -149,13 +150,14 @@ def verify_grants(moduli, batch, begin: int, end: int, n_threads: int = 8):
     return flags, ts
 
 
-def tally(batch, grant_flags: np.ndarray, grant_ts: np.ndarray, replication_factor: int, strict_gt: bool = True):
+def tally(batch, grant_flags: np.ndarray, grant_ts: np.ndarray, replication_factor: int, strict_gt: bool = True,
+          quorum_mode: int = 0):
     import mochi_hip as mh
 
     b = batch.normalized()
-    out = mh.Verdicts.alloc(b.n_grants, b.n_certs)
+    out = mh.Verdicts.alloc(b.n_grants, b.n_certs, b.n_ops)
     bc, vc = b.to_c(), out.to_c()
-    p = mh.Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+    p = mh.params(replication_factor, strict_gt, quorum_mode)
     f = np.ascontiguousarray(grant_flags, np.uint8)
     t = np.ascontiguousarray(grant_ts, np.int64)
     rc = lib().oracle_tally(ctypes.byref(bc), ctypes.byref(p), f.ctypes.data, t.ctypes.data, ctypes.byref(vc))
@@ -250,21 +252,29 @@ def w2_decode(wb, ids, id_off):
         sig=arr(b.sig, N * 256, np.uint8, (N, 256)), signer=arr(b.signer, N, np.uint16),
         grant_key=arr(b.grant_key, N, np.uint8), cert_grant_off=arr(b.cert_grant_off, C + 1, np.uint32),
         cert_op_off=arr(b.cert_op_off, C + 1, np.uint32), op_key=arr(b.op_key, O, np.uint8),
-        op_flags=arr(b.op_flags, O, np.uint8), msg_status=arr(d.msg_status, C, np.uint8))
+        op_flags=arr(b.op_flags, O, np.uint8), msg_status=arr(d.msg_status, C, np.uint8),
+        cert_mg_off=arr(b.cert_mg_off, C + 1, np.uint32), mg_grant_off=arr(b.mg_grant_off, b.n_mgs + 1, np.uint32),
+        op_key_off=arr(b.op_key_off, O, np.uint64), op_key_len=arr(b.op_key_len, O, np.uint32),
+        op_object_ts=arr(b.op_object_ts, O, np.int64))
     lib().oracle_w2_free(ctypes.addressof(d))
     return out
 
 
-def verify_write2(moduli, ids, id_off, wb, replication_factor: int, strict_gt: bool, n_threads: int = 8):
+def verify_write2(moduli, ids, id_off, wb, replication_factor: int, strict_gt: bool, n_threads: int = 8,
+                  quorum_mode: int = 0):
     import mochi_hip as mh
 
     mod = np.frombuffer(b"".join(bytes(m) for m in moduli), np.uint8).copy()
     wc, keep = _w2_c(wb)
     M = wb.n_msgs
-    out = mh.Verdicts.alloc(0, M)
+    O = int(wb.op_flags_off[-1]) if wb.op_flags_off is not None else 0
+    out = mh.Verdicts.alloc(0, M, O)
     vc = out.to_c()
     vc.grant_valid_bits = vc.grant_flags = vc.grant_ts = None
-    p = mh.Params_C(replication_factor=replication_factor, strict_gt=1 if strict_gt else 0)
+    if wb.op_flags_off is None:
+        vc.op_decision = vc.op_g0 = vc.op_ts = None
+        out.op_decision = out.op_g0 = out.op_ts = None
+    p = mh.params(replication_factor, strict_gt, quorum_mode)
     st = np.zeros(max(M, 1), np.uint8)
     rc = lib().oracle_verify_write2(mod.ctypes.data, len(moduli), ids.ctypes.data, id_off.ctypes.data,
                                     ctypes.addressof(wc), ctypes.addressof(p), ctypes.addressof(vc), st.ctypes.data,

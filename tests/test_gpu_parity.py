@@ -14,6 +14,7 @@ import mochi_hip as mh
 import oracle_ffi as O
 import workload as W
 from cases import build_case_batch, grouped_cases, moduli_for
+from test_oracle_golden import check_case_verdicts
 
 pytestmark = pytest.mark.gpu
 
@@ -56,6 +57,9 @@ def assert_same(g: mh.Verdicts, o: mh.Verdicts, what=""):
     np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits, err_msg=f"cert_accept_bits {what}")
     np.testing.assert_array_equal(g.cert_reason, o.cert_reason, err_msg=f"cert_reason {what}")
     np.testing.assert_array_equal(g.cert_fail_op, o.cert_fail_op, err_msg=f"cert_fail_op {what}")
+    for k in ("op_decision", "op_g0", "op_ts"):
+        if getattr(g, k) is not None and getattr(o, k) is not None:
+            np.testing.assert_array_equal(getattr(g, k), getattr(o, k), err_msg=f"{k} {what}")
 
 
 def test_rsa_public_op_matches_python_pow():
@@ -146,18 +150,22 @@ def test_rsa_golden_vectors_gpu(golden_dir):
     ver.close()
 
 
+@pytest.mark.parametrize("explicit_mg", [True, False])
 @pytest.mark.parametrize("key", sorted(grouped_cases().keys()))
-def test_cert_branch_cases_gpu(key):
-    R, strict = key
-    cases = grouped_cases()[key]
-    batch, reason, fail_op = build_case_batch(cases, W.load_keys(R))
+def test_cert_branch_cases_gpu(key, explicit_mg):
+    """Every branch fixture on the device: GPU == oracle array for array (grant flags,
+    timestamps, accept bits, reasons, failing ops, per-op decisions / g0 / ts) and
+    both == the hand-derived expectations."""
+    R, strict, qm = key
+    cases = grouped_cases(explicit_mg).get(key)
+    if not cases:
+        pytest.skip("every case of this group needs explicit MultiGrants")
+    batch, ex = build_case_batch(cases, W.load_keys(R), explicit_mg)
     ver = mh.Verifier(moduli_for(R), 0)
-    g = ver.verify(batch, R, bool(strict))
-    o = O.verify_batch(moduli_for(R), batch, R, bool(strict), 4)
+    g = ver.verify(batch, R, bool(strict), quorum_mode=qm)
+    o = O.verify_batch(moduli_for(R), batch, R, bool(strict), 4, quorum_mode=qm)
     assert_same(g, o, str(key))
-    for i, c in enumerate(cases):
-        assert g.cert_reason[i] == reason[i], (c["name"], c["why"])
-        assert g.cert_fail_op[i] == fail_op[i], c["name"]
+    check_case_verdicts(g, cases, ex, f"gpu mg={explicit_mg}")
     ver.close()
 
 

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
-from cases import build_case_batch, grouped_cases, moduli_for
+from cases import build_case_batch, grouped_cases, load_cases, moduli_for
 from workload import encode_grant, load_keys
 
 
@@ -87,17 +87,43 @@ def test_server_majority_restatement():
     assert [O.server_majority(r) for r in (4, 5, 6, 7, 10)] == [3, 3, 5, 5, 7]
 
 
-@pytest.mark.parametrize("key", sorted(grouped_cases().keys()))
-def test_cert_branch_cases(key):
-    R, strict = key
-    cases = grouped_cases()[key]
-    pems = load_keys(R)
-    batch, reason, fail_op = build_case_batch(cases, pems)
-    v = O.verify_batch(moduli_for(R), batch, R, bool(strict), 2)
+def check_case_verdicts(v, cases, ex, what=""):
+    """Verdicts (oracle or device) against the hand-derived expectations of cert_cases.json."""
+    op = 0
     for i, c in enumerate(cases):
-        assert v.cert_reason[i] == reason[i], (c["name"], v.cert_reason[i], c["why"])
-        assert v.cert_fail_op[i] == fail_op[i], (c["name"], v.cert_fail_op[i])
-        assert bool(v.cert_accept[i]) == (reason[i] == 0), c["name"]
+        n = len(c["ops"])
+        assert v.cert_reason[i] == ex.reason[i], (what, c["name"], v.cert_reason[i], c["why"])
+        assert v.cert_fail_op[i] == ex.fail_op[i], (what, c["name"], v.cert_fail_op[i])
+        assert bool(v.cert_accept[i]) == (ex.reason[i] == 0), (what, c["name"])
+        np.testing.assert_array_equal(v.op_decision[op:op + n], ex.decisions[op:op + n], err_msg=f"{what} {c['name']}")
+        np.testing.assert_array_equal(v.op_g0[op:op + n], ex.g0[op:op + n], err_msg=f"{what} {c['name']} g0")
+        np.testing.assert_array_equal(v.op_ts[op:op + n], ex.op_ts[op:op + n], err_msg=f"{what} {c['name']} ts")
+        op += n
+    assert op == v.op_decision.shape[0]
+
+
+@pytest.mark.parametrize("explicit_mg", [True, False])
+@pytest.mark.parametrize("key", sorted(grouped_cases().keys()))
+def test_cert_branch_cases(key, explicit_mg):
+    """Oracle restatement vs the per-branch expectations (reason, failing op, per-op
+    read/apply decision, g0 and its timestamp), with MultiGrant boundaries given
+    explicitly and -- where they are runs of one signer -- left to the default."""
+    R, strict, qm = key
+    cases = grouped_cases(explicit_mg).get(key)
+    if not cases:
+        pytest.skip("every case of this group needs explicit MultiGrants")
+    batch, ex = build_case_batch(cases, load_keys(R), explicit_mg)
+    v = O.verify_batch(moduli_for(R), batch, R, bool(strict), 2, quorum_mode=qm)
+    check_case_verdicts(v, cases, ex, f"oracle mg={explicit_mg}")
+
+
+def test_cert_cases_cover_every_reason_and_decision():
+    cases = load_cases()
+    reasons = {c["reason"] for c in cases}
+    assert reasons == {0, 1, 2, 3, 4, 5, 6, 8, 9, 10}  # 7 (UNDECIDED) is wire-path only
+    decisions = {d for c in cases for d in c["decisions"]}
+    assert decisions == {0, 1, 2, 3, 4}
+    assert {c.get("quorum_mode", 0) for c in cases} == {0, 1, 2, 3}
 
 
 def test_write1_uniform_restatement():

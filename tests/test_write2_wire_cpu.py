@@ -85,6 +85,15 @@ def check_decode_against_golden(v, d, wire, ids):
     n = len(exp_slots)
     assert len(got_slots) == n, v["name"]
     assert all((got_slots[i] == got_slots[j]) == (exp_slots[i] == exp_slots[j]) for i in range(n) for j in range(n)), v["name"]
+    # Operation.action (last value wins) / empty operand1 -> MOCHI_OP_NOT_WRITE; the op key slices
+    for j, (k, act) in enumerate(zip(content["ops"], content["actions"])):
+        notw = act not in (1, 2) or k == ""
+        assert bool(d["op_flags"][j] & 0x10) == notw, (v["name"], j, act)
+        o, n = int(d["op_key_off"][j]), int(d["op_key_len"][j])
+        assert wire[o:o + n].decode() == k, (v["name"], j)
+    # MultiGrant boundaries: one per certificate entry (first occurrence), its grants
+    assert d["cert_mg_off"].tolist() == [0, len(order["certs"])], v["name"]
+    assert np.diff(d["mg_grant_off"]).tolist() == [len(x) for x in order["grants"]], v["name"]
     g = 0
     assert sum(len(x) for x in order["grants"]) == int(d["cert_grant_off"][1]), v["name"]
     for ci, ckey in enumerate(order["certs"]):

@@ -12,7 +12,7 @@ from test_write2_wire_cpu import _golden, check_decode_against_golden
 pytestmark = pytest.mark.gpu
 
 KEYS = ("grant_off", "grant_len", "sig", "signer", "grant_key", "cert_grant_off", "cert_op_off", "op_key",
-        "op_flags", "msg_status")
+        "op_flags", "msg_status", "cert_mg_off", "mg_grant_off", "op_key_off", "op_key_len")
 
 
 @pytest.fixture(scope="module")
@@ -21,8 +21,29 @@ def pool4():
 
 
 @pytest.fixture(scope="module")
+def pool4k2_wire():
+    return W.build_pool(R=4, k=2, P=256, P_f=64)
+
+
+@pytest.fixture(scope="module")
 def pool7k2():
     return W.build_pool(R=7, k=2, P=256, P_f=64)
+
+
+def grant_ts_of_ops(s):
+    """Per op: the timestamp of its certificate's first grant for the op's key slot
+    (parsed by the oracle); stored-certificate timestamps are drawn around it."""
+    b = s.batch
+    out = np.zeros(b.n_ops, np.int64)
+    for c in range(b.n_certs):
+        g0, g1 = int(b.cert_grant_off[c]), int(b.cert_grant_off[c + 1])
+        for o in range(int(b.cert_op_off[c]), int(b.cert_op_off[c + 1])):
+            for g in range(g0, g1):
+                if b.grant_key[g] == b.op_key[o]:
+                    gb = b.grant_bytes[int(b.grant_off[g]):int(b.grant_off[g]) + int(b.grant_len[g])].tobytes()
+                    out[o] = O.grant_parse(gb)["timestamp"]
+                    break
+    return out
 
 
 def _ver(pool):
@@ -88,6 +109,45 @@ def test_wire_verdicts_equal_soa_verdicts(pool4, strict):
     d = ver.decode_write2(wb)
     np.testing.assert_array_equal(d["signer"], s.batch.signer)
     np.testing.assert_array_equal(d["sig"], s.batch.sig)
+    # per-op outputs: wire path == SoA path == oracle
+    for k in ("op_decision", "op_g0", "op_ts"):
+        np.testing.assert_array_equal(getattr(g, k), getattr(soa, k), err_msg=k)
+        np.testing.assert_array_equal(getattr(g, k), getattr(o, k), err_msg=k)
+    ver.close()
+
+
+@pytest.mark.parametrize("chunk", [64, 0])
+def test_wire_stored_state_and_per_op_outputs(pool4k2_wire, chunk):
+    """SVOC state inputs through the wire path (op flags HAS_CURRENT_C / CURRENT_C_BAD /
+    NOT_WRITE + op_object_ts): read vs apply branch, stored-certificate throws, per-op
+    decisions / g0 / ts -- device == oracle, on the chunked host pipeline (64-grant
+    chunks) and in one piece."""
+    pool = pool4k2_wire
+    ver = _ver(pool)
+    if chunk:
+        ver.set_chunk_grants(chunk)
+    rng = np.random.default_rng(99)
+    s = W.make_batch(pool, 1500, first_cert=77)
+    wb = W.encode_wire_batch(s)
+    O_ = int(wb.op_flags_off[-1])
+    wb.op_flags = rng.choice(np.array([3, 7, 7, 7, 15, 1, 2, 23, 19, 11], np.uint8), O_)
+    ts = np.zeros(O_, np.int64)
+    # stored timestamps around each op's grant timestamp (read iff stored > g0.ts)
+    base = grant_ts_of_ops(s)
+    ts[:] = base + rng.integers(-2, 3, O_)
+    wb.op_object_ts = ts
+    ids, off = W.server_id_table(4)
+    for strict in (True, False):
+        g, st = ver.verify_write2(wb, 4, strict)
+        o, ost = O.verify_write2(pool.moduli, ids, off, wb, 4, strict)
+        np.testing.assert_array_equal(st, ost)
+        np.testing.assert_array_equal(g.cert_reason, o.cert_reason)
+        np.testing.assert_array_equal(g.cert_fail_op, o.cert_fail_op)
+        np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits)
+        for k in ("op_decision", "op_g0", "op_ts"):
+            np.testing.assert_array_equal(getattr(g, k), getattr(o, k), err_msg=k)
+        assert {1, 2, 3, 4} <= set(np.unique(g.op_decision).tolist())
+        assert {0, 9, 10} <= set(np.unique(g.cert_reason).tolist())
     ver.close()
 
 
@@ -112,7 +172,7 @@ def _mutate(rng, s, c, ids):
         gb = b.grant_bytes[int(b.grant_off[g]):int(b.grant_off[g]) + int(b.grant_len[g])].tobytes()
         mgs.setdefault(int(b.signer[g]), []).append((W.grant_object_id(gb), gb, b.sig[g].tobytes()))
     order = list(mgs)
-    kind = int(rng.integers(0, 9))
+    kind = int(rng.integers(0, 10))
     if kind == 1:
         rng.shuffle(order)  # MultiGrant wire order decides g0
     enc = []
@@ -132,6 +192,9 @@ def _mutate(rng, s, c, ids):
     ops = [W.encode_operation(2, o) for o, _, _ in mgs[order[0]]]
     if kind == 6:
         ops = ops + ops  # ops repeating a key (multiplicity)
+    if kind == 9:  # READ / DELETE / unknown actions, an empty operand1 -> MOCHI_OP_NOT_WRITE or not
+        ops = [W.encode_operation(int(rng.choice([0, 1, 2, 5])), o) for o, _, _ in mgs[order[0]]]
+        ops.append(W.encode_operation(2, ""))
     m = W.encode_write2(enc, ops)
     if kind == 7 and len(m) > 8:
         i = int(rng.integers(0, len(m)))
