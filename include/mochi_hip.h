@@ -468,6 +468,16 @@ int mochi_sign_batch(mochi_signer* s, const uint8_t* grant_bytes, uint64_t grant
 /* Device memory, asynchronous on `stream`. */
 int mochi_sign_batch_device(mochi_signer* s, const uint8_t* grant_bytes, const uint64_t* grant_off,
                             const uint32_t* grant_len, uint32_t n, uint8_t* sig_out, void* stream);
+/* Every signature is verified with the signer's public key before it is
+ * released (same stream, ~2 % of the signing cost): a transient fault in one
+ * RSA-CRT half would otherwise publish s with gcd(s^e - EM, n) = a prime factor.
+ * A failing signature is written as 256 zero bytes (it verifies nowhere).
+ * mochi_signer_rejected waits for the device and returns (and clears) the
+ * number withheld since the last call. */
+int mochi_signer_rejected(mochi_signer* s, uint64_t* rejected);
+/* Test hook: corrupt the CRT half m_p of grant `grant_index` of every later call
+ * (0xFFFFFFFF = off), to show the fault check withholding it. */
+int mochi_signer_set_fault(mochi_signer* s, uint32_t grant_index);
 
 /* ------------------------------------------------------------------------
  * Micro-batcher: the blocking per-request call the Java handler keeps

@@ -1481,6 +1481,10 @@ struct mochi_signer {
   std::mutex mu;
   DevBuf dev_in, dev_sig;
   PinnedBuf pin_in, pin_out;
+  // fault check: the verify path under the signer's own public key
+  mochi_ctx* check = nullptr;
+  DevBuf zeros, flags, misc;  // signer index / key slot zeros, SIG_OK flags, [0] rejected [1..] CSR zeros
+  uint32_t fault_idx = 0xFFFFFFFFu;
 };
 
 namespace {
@@ -1581,6 +1585,18 @@ mochi_signer* mochi_signer_create(int device, const char* pem) {
     mochi_signer_destroy(s);
     return nullptr;
   }
+  uint8_t n_be[MOCHI_RSA_BYTES];
+  if (mochi_pem_modulus(pem, n_be) != MOCHI_OK ||
+      !(s->check = mochi_ctx_create(device, n_be, 1, MOCHI_RSA_BYTES, MOCHI_RSA_E))) {
+    fail(MOCHI_EINVAL, "signer: public-key check context failed");
+    mochi_signer_destroy(s);
+    return nullptr;
+  }
+  if (s->misc.ensure(256) || hipMemset(s->misc.p, 0, 256) != hipSuccess) {
+    fail(MOCHI_EHIP, "signer scratch");
+    mochi_signer_destroy(s);
+    return nullptr;
+  }
   return s;
 }
 
@@ -1595,8 +1611,68 @@ void mochi_signer_destroy(mochi_signer* s) {
     (void)hipFree(s->d_key);
   }
   if (s->stream) (void)hipStreamDestroy(s->stream);
+  if (s->check) mochi_ctx_destroy(s->check);
   delete s;
   (void)hipSetDevice(save);
+}
+
+}  // extern "C"
+
+namespace {
+// Verify n freshly made signatures with the signer's public key on the same
+// stream (k_grant_prep + k_rsa_pow + k_rsa_final, ~1/50 of the signing work)
+// and withhold every one that fails (RSA-CRT fault attack, Boneh-DeMillo-Lipton).
+int signer_check(mochi_signer* s, const uint8_t* grant_bytes, const uint64_t* grant_off, const uint32_t* grant_len,
+                 uint32_t n, uint8_t* sig, hipStream_t st) {
+  if (!n) return MOCHI_OK;
+  int rc;
+  if ((rc = s->zeros.ensure(2 * (size_t)n)) || (rc = s->flags.ensure(n))) return rc;
+  HIP_TRY(hipMemsetAsync(s->zeros.p, 0, 2 * (size_t)n, st));
+  mochi_batch db;
+  memset(&db, 0, sizeof db);
+  db.n_grants = n;
+  db.grant_bytes = grant_bytes;
+  db.grant_off = grant_off;
+  db.grant_len = grant_len;
+  db.sig = sig;
+  db.signer = s->zeros.as<uint16_t>();
+  db.grant_key = s->zeros.as<uint8_t>();
+  uint32_t* misc = s->misc.as<uint32_t>();
+  db.cert_grant_off = misc + 1;  // one zero: no certificates
+  db.cert_op_off = misc + 1;
+  mochi_params p = {1, 1, 0, 0};
+  mochi_verdicts dv;
+  memset(&dv, 0, sizeof dv);
+  dv.grant_flags = s->flags.as<uint8_t>();
+  dv.cert_accept_bits = misc + 2;
+  if ((rc = run_device(s->check, &db, &p, &dv, st))) return rc;
+  HIP_TRY(mochi::launch_withhold(s->flags.as<uint8_t>(), n, sig, misc, st));
+  return MOCHI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int mochi_signer_set_fault(mochi_signer* s, uint32_t grant_index) {
+  if (!s) return fail(MOCHI_EINVAL, "null signer");
+  std::lock_guard<std::mutex> lk(s->mu);
+  s->fault_idx = grant_index;
+  return MOCHI_OK;
+}
+
+int mochi_signer_rejected(mochi_signer* s, uint64_t* rejected) {
+  if (!s || !rejected) return fail(MOCHI_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  int save = 0;
+  (void)hipGetDevice(&save);
+  uint32_t v = 0;
+  const bool ok = hipSetDevice(s->device) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+                  hipMemcpy(&v, s->misc.p, 4, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemset(s->misc.p, 0, 4) == hipSuccess;
+  (void)hipSetDevice(save);
+  if (!ok) return fail(MOCHI_EHIP, "signer counter read failed");
+  *rejected = v;
+  return MOCHI_OK;
 }
 
 int mochi_sign_batch_device(mochi_signer* s, const uint8_t* grant_bytes, const uint64_t* grant_off,
@@ -1606,10 +1682,15 @@ int mochi_sign_batch_device(mochi_signer* s, const uint8_t* grant_bytes, const u
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(s->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice");
-  const hipError_t e = mochi::launch_rsa_sign(grant_bytes, grant_off, grant_len, n, s->d_key, sig_out,
+  const hipError_t e = mochi::launch_rsa_sign(grant_bytes, grant_off, grant_len, n, s->d_key, sig_out, s->fault_idx,
                                               (hipStream_t)stream);
+  int rc = e == hipSuccess ? MOCHI_OK : fail(MOCHI_EHIP, "k_rsa_sign: %s", hipGetErrorString(e));
+  if (!rc) {
+    std::lock_guard<std::mutex> ck(s->check->mu);
+    rc = signer_check(s, grant_bytes, grant_off, grant_len, n, sig_out, (hipStream_t)stream);
+  }
   (void)hipSetDevice(save);
-  return e == hipSuccess ? MOCHI_OK : fail(MOCHI_EHIP, "k_rsa_sign: %s", hipGetErrorString(e));
+  return rc;
 }
 
 int mochi_sign_batch(mochi_signer* s, const uint8_t* grant_bytes, uint64_t grant_bytes_len, const uint64_t* grant_off,
@@ -1640,7 +1721,13 @@ int mochi_sign_batch(mochi_signer* s, const uint8_t* grant_bytes, uint64_t grant
   hipError_t e = hipMemcpyAsync(din, pin, total, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = mochi::launch_rsa_sign(din, (const uint64_t*)(din + o_off), (const uint32_t*)(din + o_len), n, s->d_key,
-                               s->dev_sig.as<uint8_t>(), st);
+                               s->dev_sig.as<uint8_t>(), s->fault_idx, st);
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> ck(s->check->mu);
+    if (signer_check(s, din, (const uint64_t*)(din + o_off), (const uint32_t*)(din + o_len), n,
+                     s->dev_sig.as<uint8_t>(), st) != MOCHI_OK)
+      e = hipErrorUnknown;
+  }
   if (e == hipSuccess) e = hipMemcpyAsync(s->pin_out.p, s->dev_sig.p, sig_bytes, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e == hipSuccess) memcpy(sig_out, s->pin_out.p, sig_bytes);

@@ -120,7 +120,9 @@ void sign_key_set(void* dst, const uint32_t* p, const uint32_t* q, const uint32_
                   const uint32_t* qinv_r, const uint32_t* dp, const uint32_t* dq, const uint32_t* cpad, uint32_t p0inv,
                   uint32_t q0inv, uint32_t dp_bits, uint32_t dq_bits);
 hipError_t launch_rsa_sign(const uint8_t* blob, const uint64_t* goff, const uint32_t* glen, uint32_t n,
-                           const void* key, uint8_t* sig, hipStream_t stream);
+                           const void* key, uint8_t* sig, uint32_t fault_idx, hipStream_t stream);
+// Zero every signature whose flags lack MOCHI_GRANT_SIG_OK and count them.
+hipError_t launch_withhold(const uint8_t* flags, uint32_t n, uint8_t* sig, uint32_t* rejected, hipStream_t stream);
 hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t stream);
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream);
 void launch_rsa_final(const LaunchArgs& a, hipStream_t stream);

@@ -437,10 +437,28 @@ __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t* __restrict__ f
   if (lane == 0 && wbase + 1 < nwords) bits[wbase + 1] = (uint32_t)(b >> 32);
 }
 
+// Producer-side fault check: a signature that does not verify under the
+// signer's own public key is never released (a faulty RSA-CRT half would leak
+// a prime factor: gcd(s^e - EM, n)); it is zeroed and counted.
+__global__ __launch_bounds__(256) void k_withhold(const uint8_t* __restrict__ flags, uint32_t n, uint8_t* __restrict__ sig,
+                                                  uint32_t* __restrict__ rejected) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (flags[i] & MOCHI_GRANT_SIG_OK)) return;
+  uint4* s = (uint4*)(sig + (size_t)i * MOCHI_RSA_BYTES);
+#pragma unroll
+  for (int q = 0; q < MOCHI_RSA_BYTES / 16; q++) s[q] = make_uint4(0, 0, 0, 0);
+  atomicAdd(rejected, 1u);
+}
+
 // ---------------------------------------------------------------------------
 // Launchers (host side of this translation unit).
 // ---------------------------------------------------------------------------
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_withhold(const uint8_t* flags, uint32_t n, uint8_t* sig, uint32_t* rejected, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_withhold, dim3(cdiv(n, 256)), dim3(256), 0, st, flags, n, sig, rejected);
+  return hipGetLastError();
+}
 
 hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_pack_bits, dim3(cdiv(n, 256)), dim3(256), 0, st, flags, n, mask, bits);

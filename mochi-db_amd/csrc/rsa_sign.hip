@@ -111,7 +111,8 @@ __device__ __forceinline__ void crt_half(uint32_t (&out)[kLh], const uint32_t (&
 __global__ __launch_bounds__(256, 3) void k_rsa_sign(const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ goff,
                                                      const uint32_t* __restrict__ glen, uint32_t n,
-                                                     const SignKey* __restrict__ key, uint8_t* __restrict__ sig) {
+                                                     const SignKey* __restrict__ key, uint8_t* __restrict__ sig,
+                                                     uint32_t fault_idx) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
   uint32_t hl[10];
@@ -134,6 +135,7 @@ __global__ __launch_bounds__(256, 3) void k_rsa_sign(const uint8_t* __restrict__
   uint32_t m1[kLh], m2[kLh];
   crt_half(m1, hl, cpad, p, *as_const(&key->p0inv), as_const(key->r3p), as_const(key->dp), *as_const(&key->dp_bits));
   crt_half(m2, hl, cpad, q, *as_const(&key->q0inv), as_const(key->r3q), as_const(key->dq), *as_const(&key->dq_bits));
+  if (g == fault_idx) m1[0] ^= 1u;  // test hook (mochi_signer_set_fault): a transient fault in one CRT half
   // Garner: h = qInv (m1 - m2 mod p) mod p
   uint32_t d[kLh];
 #pragma unroll
@@ -213,10 +215,10 @@ void sign_key_set(void* dst, const uint32_t* p, const uint32_t* q, const uint32_
 }
 
 hipError_t launch_rsa_sign(const uint8_t* blob, const uint64_t* goff, const uint32_t* glen, uint32_t n,
-                           const void* key, uint8_t* sig, hipStream_t st) {
+                           const void* key, uint8_t* sig, uint32_t fault_idx, hipStream_t st) {
   if (n)
     hipLaunchKernelGGL(k_rsa_sign, dim3((n + 255) / 256), dim3(256), 0, st, blob, goff, glen, n,
-                       (const SignKey*)key, sig);
+                       (const SignKey*)key, sig, fault_idx);
   return hipGetLastError();
 }
 

@@ -181,6 +181,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_signer_destroy.argtypes = [vp]
     lib.mochi_sign_batch.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, u32, vp]
     lib.mochi_sign_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp]
+    lib.mochi_signer_rejected.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    lib.mochi_signer_set_fault.argtypes = [vp, u32]
     lib.mochi_batcher_create.restype = vp
     lib.mochi_batcher_create.argtypes = [vp, vp, u32, u32, ctypes.c_int]
     lib.mochi_batcher_verify.argtypes = [vp, vp, u32, vp, u32, vp, vp]
@@ -884,6 +886,17 @@ class DeviceSigner:
                                               sig_t.data_ptr(), stream)
         if rc != OK:
             raise MochiError(f"mochi_sign_batch_device rc={rc}: {_err(self.lib)}")
+
+    def rejected(self) -> int:
+        """Signatures withheld by the public-key fault check since the last call."""
+        v = ctypes.c_uint64()
+        if self.lib.mochi_signer_rejected(self.h, ctypes.byref(v)) != OK:
+            raise MochiError(f"mochi_signer_rejected: {_err(self.lib)}")
+        return v.value
+
+    def set_fault(self, grant_index: int) -> None:
+        """Test hook: corrupt one CRT half of grant `grant_index` (-1 = off)."""
+        self.lib.mochi_signer_set_fault(self.h, grant_index & 0xFFFFFFFF)
 
     def close(self):
         if self.h:

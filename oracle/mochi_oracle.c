@@ -449,6 +449,20 @@ int oracle_verify_grants(const uint8_t* moduli_be, uint32_t n_keys, const mochi_
   return MOCHI_OK;
 }
 
+/* Parse leg only (no signatures): MOCHI_GRANT_PARSED and Grant.timestamp of
+ * grants [begin, end) by oracle_grant_parse, so a large batch's tally can be
+ * checked against the oracle's own parse without re-verifying every signature. */
+int oracle_parse_grants(const mochi_batch* b, uint32_t begin, uint32_t end, uint8_t* grant_flags, int64_t* grant_ts) {
+  if (!b || begin > end || end > b->n_grants || !grant_flags || !grant_ts) return MOCHI_EINVAL;
+  for (uint32_t i = begin; i < end; i++) {
+    oracle_grant_view v;
+    const int ok = oracle_grant_parse(b->grant_bytes + b->grant_off[i], b->grant_len[i], &v);
+    grant_flags[i] = ok ? MOCHI_GRANT_PARSED : 0;
+    grant_ts[i] = ok ? v.timestamp : 0;
+  }
+  return MOCHI_OK;
+}
+
 /* ------------------------------------------------------------------------ */
 /* a3 + a4: the certificate verdict                                           */
 /* ------------------------------------------------------------------------ */

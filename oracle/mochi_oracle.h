@@ -77,6 +77,11 @@ int oracle_verify_batch(const uint8_t* moduli_be, uint32_t n_keys, const mochi_b
 int oracle_verify_grants(const uint8_t* moduli_be, uint32_t n_keys, const mochi_batch* batch, uint32_t begin,
                          uint32_t end, uint8_t* grant_flags, int64_t* grant_ts, int n_threads);
 
+/* Parse leg only: grant_flags[i] = MOCHI_GRANT_PARSED or 0, grant_ts[i] =
+ * Grant.timestamp, for grants [begin, end); no signature checks. */
+int oracle_parse_grants(const mochi_batch* batch, uint32_t begin, uint32_t end, uint8_t* grant_flags,
+                        int64_t* grant_ts);
+
 /* Only the tally leg, from precomputed grant_flags / grant_ts. */
 int oracle_tally(const mochi_batch* batch, const mochi_params* params, const uint8_t* grant_flags,
                  const int64_t* grant_ts, mochi_verdicts* out);

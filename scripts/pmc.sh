@@ -4,7 +4,7 @@
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/pmc"; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=(python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --headline-only --pool 1024)
+BENCH=(python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --headline-only ${BENCH_ARGS:-})
 pass() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "k_rsa|k_grant_prep|k_tally" --output-format csv \
@@ -12,7 +12,6 @@ pass() {
 }
 pass sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU
 pass sq2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_IFETCH SQ_WAVES GRBM_GUI_ACTIVE
-pass sqc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_TC_INST_REQ
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 echo "pmc passes done"

@@ -48,14 +48,15 @@ def load_pass(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r01")
-    ap.add_argument("--grants", type=int, default=998748)
+    ap.add_argument("--grants", type=int, default=15980098)
+    ap.add_argument("--what", default="bench.py --headline-only --steps 2 --warmup 1 (C4: 16M grants, R=4)")
     a = ap.parse_args()
     per = collections.defaultdict(dict)
-    for p in ("sq1", "sq2", "sqc", "fetch", "write"):
+    for p in ("sq1", "sq2", "fetch", "write"):
         for k, d in load_pass(p).items():
             per[k].update(d)
-    out = {"source": "rocprofv3 --pmc, scripts/pmc.sh (bench.py --steps 2 --warmup 1, 1M grants, R=4); "
-                     "values are per dispatch, averaged over dispatches", "kernels": {}}
+    out = {"source": f"rocprofv3 --pmc, scripts/pmc.sh ({a.what}); values are per dispatch of the largest grid "
+                     "(the headline launch), averaged over those dispatches", "kernels": {}}
     for k, d in per.items():
         e = dict(d)
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
@@ -87,6 +88,8 @@ def main():
                        "algorithmic_bytes_per_launch": algo,
                        "note": "FETCH_SIZE*2 (gfx950 16-B/lane correction) + WRITE_SIZE, KiB->B"}, f, indent=1)
     ks = os.path.join(ROOT, "gpurun_out", "prof_kt", "run_kernel_stats.csv")
+    found = glob.glob(os.path.join(ROOT, "gpurun_out", "prof_kt", "**", "*kernel_stats.csv"), recursive=True)
+    ks = found[0] if found else ks
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(ROOT, "profiles", f"{a.round}_kernel_stats.csv"))
     print(json.dumps({k: {kk: v for kk, v in e.items() if not kk.startswith("SQ")} for k, e in out["kernels"].items()},

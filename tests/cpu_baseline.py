@@ -44,7 +44,18 @@ def _wait_for(path, timeout_s=900):
         time.sleep(0.2)
 
 
-def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=None, batch_file=None):
+def cpu_share():
+    """Worker count: every CPU this process may run on, capped by the job's CPU
+    share when the host declares one (the GPU pool gives a 1-GPU job 16 CPUs and
+    exports OMP_NUM_THREADS=16; nproc there reports the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    n = min(aff, int(share)) if share and share.isdigit() and int(share) > 0 else aff
+    return max(1, n), aff, os.cpu_count() or aff, share
+
+
+def run(R, k, cache_dir, n_certs, procs, seconds, runs, strict, flags_out=None, batch_file=None, stream="C4",
+        pool_size=4096):
     import numpy as np
 
     import mochi_hip as mh
@@ -59,6 +70,7 @@ def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=N
         moduli = [mh.pem_modulus(p) for p in W.load_keys(R)]
         probe = W.head_certs(full, 256)
         make = lambda n: W.head_certs(full, n)
+        n_certs = min(n_certs, full.batch.n_certs)
     else:
         pool = W.build_pool(R=R, k=k, P=pool_size, P_f=256, cache_dir=cache_dir)
         moduli = pool.moduli
@@ -68,7 +80,7 @@ def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=N
     t0 = time.perf_counter()
     O.verify_grants(moduli, probe.batch, 0, probe.batch.n_grants, 1)
     rate1 = probe.batch.n_grants / max(1e-6, time.perf_counter() - t0)
-    want = int(rate1 * procs * seconds / (R * k))
+    want = int(rate1 * seconds / (R * k))  # `seconds` of CPU work (core-seconds) per run
     n = max(64, min(n_certs, want))
     s = make(n)
     N = s.batch.n_grants
@@ -76,16 +88,19 @@ def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=N
     chunks = max(procs * 4, 1)
     ranges = [(N * i // chunks, N * (i + 1) // chunks) for i in range(chunks)]
     ctx = mp.get_context("fork")
+    times = []
     with ctx.Pool(procs) as p:
         p.map(_work, ranges[:procs])  # warm the workers (library load, key setup)
-        t0 = time.perf_counter()
-        flags = np.zeros(N, np.uint8)
-        ts = np.zeros(N, np.int64)
-        for b, e, f, t in p.imap_unordered(_work, ranges):
-            flags[b:e] = f
-            ts[b:e] = t
-        v = O.tally(s.batch, flags, ts, R, strict)
-        dt = time.perf_counter() - t0
+        for _ in range(max(1, runs)):
+            t0 = time.perf_counter()
+            flags = np.zeros(N, np.uint8)
+            ts = np.zeros(N, np.int64)
+            for b, e, f, t in p.imap_unordered(_work, ranges):
+                flags[b:e] = f
+                ts[b:e] = t
+            v = O.tally(s.batch, flags, ts, R, strict)
+            times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
     if flags_out:
         np.savez(flags_out, grant_flags=flags, cert_reason=v.cert_reason, cert_accept_bits=v.cert_accept_bits)
     cpu = ""
@@ -97,15 +112,21 @@ def run(R, k, pool_size, cache_dir, n_certs, procs, seconds, strict, flags_out=N
                     break
     except OSError:
         pass
+    _, aff, nproc, share = cpu_share()
     return {
         "value": round(N / dt, 1),
         "unit": "grants/s",
         "cores": procs,
         "kind": "port",
-        "sample": f"first {n} certificates ({N} grants) of the C2 stream{' (unique grants)' if batch_file else ''}; OpenSSL 3.0.2 SHA-256 + RSA-2048 PKCS#1 "
-                  f"v1.5 verify per grant + restated InMemoryDataStore.java:576-640 tally; {procs} worker processes "
-                  f"on '{cpu}'; {dt:.2f} s wall x {procs} processes = {dt * procs:.1f} core-seconds of CPU work",
+        "sample": f"first {n} certificates ({N} grants) of the {stream} stream (unique grants); OpenSSL 3.0.2 SHA-256 + "
+                  f"RSA-2048 PKCS#1 v1.5 verify per grant + restated InMemoryDataStore.java:576-640 tally; {procs} "
+                  f"worker processes on '{cpu}' (nproc {nproc}, affinity {aff}, job CPU share "
+                  f"OMP_NUM_THREADS={share}); median of {len(times)} runs, {dt:.2f} s wall each = "
+                  f"{dt * procs:.1f} core-seconds",
+        "runs_s": [round(x, 3) for x in times],
         "single_core_grants_per_s": round(rate1, 1),
+        "whole_host_extrapolated_grants_per_s": round(N / dt / procs * nproc, 1),
+        "nproc": nproc,
         "n_certs": n,
         "n_grants": N,
     }
@@ -119,14 +140,16 @@ def main():
     ap.add_argument("--cache-dir", default="/tmp/mochi_bench_cache")
     ap.add_argument("--max-certs", type=int, default=250_000)
     ap.add_argument("--procs", type=int, default=0)
-    ap.add_argument("--seconds", type=float, default=12.0)
+    ap.add_argument("--seconds", type=float, default=12.0, help="CPU work (core-seconds) per timed run")
+    ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--client-predicate", action="store_true")
     ap.add_argument("--flags-out", default=None)
     ap.add_argument("--batch-file", default=None, help="wait for and load this saved batch (bench's unique stream)")
+    ap.add_argument("--stream", default="C4")
     a = ap.parse_args()
-    procs = a.procs or max(1, min(16, len(os.sched_getaffinity(0))))
-    res = run(a.replication, a.ops_per_txn, a.pool, a.cache_dir, a.max_certs, procs, a.seconds,
-              not a.client_predicate, a.flags_out, a.batch_file)
+    procs = a.procs or cpu_share()[0]
+    res = run(a.replication, a.ops_per_txn, a.cache_dir, a.max_certs, procs, a.seconds, a.runs,
+              not a.client_predicate, a.flags_out, a.batch_file, a.stream, a.pool)
     print(json.dumps(res), flush=True)
 
 

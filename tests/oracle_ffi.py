@@ -40,6 +40,7 @@ def lib():
         L.oracle_verify_batch.argtypes = [vp, u32, vp, vp, vp, ctypes.c_int]
         L.oracle_verify_grants.argtypes = [vp, u32, vp, u32, u32, vp, vp, ctypes.c_int]
         L.oracle_tally.argtypes = [vp, vp, vp, vp, vp]
+        L.oracle_parse_grants.argtypes = [vp, u32, u32, vp, vp]
         L.oracle_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
         L.oracle_write1_uniform.argtypes = [u32, vp, vp]
         L.oracle_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -147,6 +148,16 @@ def verify_grants(moduli, batch, begin: int, end: int, n_threads: int = 8):
     rc = lib().oracle_verify_grants(m.ctypes.data, len(moduli), ctypes.byref(bc), begin, end, flags.ctypes.data,
                                     ts.ctypes.data, n_threads)
     assert rc == 0
+    return flags, ts
+
+
+def parse_grants(batch):
+    """The oracle's own Grant parse of every grant: (PARSED flags, timestamps)."""
+    b = batch.normalized()
+    bc = b.to_c()
+    flags = np.zeros(b.n_grants, np.uint8)
+    ts = np.zeros(b.n_grants, np.int64)
+    assert lib().oracle_parse_grants(ctypes.byref(bc), 0, b.n_grants, flags.ctypes.data, ts.ctypes.data) == 0
     return flags, ts
 
 

@@ -58,3 +58,38 @@ def test_device_signed_grants_verify_on_device():
     g = ver.verify(b, 4, True)
     assert (g.grant_flags & 1).all()
     ver.close()
+
+
+def test_crt_fault_is_withheld():
+    """A fault in one RSA-CRT half (injected into grant 5's m_p) must never reach the
+    caller: the public-key check after k_rsa_sign zeroes that signature and counts it;
+    every other signature is still OpenSSL's.  Host and device entry points."""
+    import torch
+
+    pem = W.load_keys(2)[1]
+    blob, off, ln = _grants(300, seed=21)
+    ref = mh.sign_grants(pem, blob, off, ln, 8)
+    s = mh.DeviceSigner(pem, 0)
+    assert s.rejected() == 0
+    s.set_fault(5)
+    got = s.sign(blob, off, ln)
+    assert s.rejected() == 1
+    assert not got[5].any()
+    keep = np.arange(300) != 5
+    np.testing.assert_array_equal(got[keep], ref[keep])
+    # device entry point, fault at the last grant
+    s.set_fault(299)
+    d = torch.device("cuda", 0)
+    bt = torch.from_numpy(blob).to(d)
+    ot = torch.from_numpy(off.view(np.int64)).to(d)
+    lt = torch.from_numpy(ln.view(np.int32)).to(d)
+    st = torch.empty((300, 256), dtype=torch.uint8, device=d)
+    s.sign_device(bt, ot, lt, 300, st, torch.cuda.current_stream().cuda_stream)
+    assert s.rejected() == 1
+    g2 = st.cpu().numpy()
+    assert not g2[299].any()
+    np.testing.assert_array_equal(g2[:299], ref[:299])
+    s.set_fault(-1)
+    np.testing.assert_array_equal(s.sign(blob, off, ln), ref)
+    assert s.rejected() == 0
+    s.close()
