@@ -21,6 +21,7 @@
 #include "../../include/mochi_hip.h"
 #include "kernels.h"
 #include "mont.h"
+#include "w2_host.h"
 
 namespace {
 
@@ -186,6 +187,7 @@ struct mochi_ctx {
   // Write2 wire path: server-id table + decode scratch
   DevBuf ids, id_off;
   uint32_t n_ids = 0;
+  std::vector<std::string> server_ids;  // host copy for the fallback decoder (w2_host.cpp)
   DevBuf w2_cnt, w2_status, w2_scan, w2_goff, w2_glen, w2_sig, w2_signer, w2_gkey, w2_okey, w2_oflags, w2_sigsrc,
       w2_mgo, w2_ots, w2_okoff, w2_oklen;
   PinnedBuf w2_tot;
@@ -955,7 +957,11 @@ int mochi_ctx_set_server_ids(mochi_ctx* c, const uint8_t* ids, const uint32_t* i
   if (!rc && nb && hipMemcpy(c->ids.p, ids, nb, hipMemcpyHostToDevice) != hipSuccess) rc = fail(MOCHI_EHIP, "copy ids");
   if (!rc && hipMemcpy(c->id_off.p, id_off, 4 * ((size_t)n_ids + 1), hipMemcpyHostToDevice) != hipSuccess)
     rc = fail(MOCHI_EHIP, "copy id_off");
-  if (!rc) c->n_ids = n_ids;
+  if (!rc) {
+    c->n_ids = n_ids;
+    c->server_ids.clear();
+    for (uint32_t i = 0; i < n_ids; i++) c->server_ids.emplace_back((const char*)ids + id_off[i], id_off[i + 1] - id_off[i]);
+  }
   (void)hipSetDevice(save);
   return rc;
 }
@@ -1013,6 +1019,125 @@ void mochi_write2_decoded_free(mochi_write2_decoded* d) {
   free(d->op_key_off);
   free(d->op_key_len);
   memset(d, 0, sizeof *d);
+}
+
+// ---- Write2 wire path: the messages the device decoder declines -------------
+//
+// MOCHI_MSG_FALLBACK messages (repeated / merged fields, non-canonical Grant
+// bytes, more than 32 MultiGrants or 64 grants per MultiGrant) are decoded on
+// the host with full protobuf-java semantics (w2_host.cpp) into an SoA batch and
+// verified through the same device path as every other certificate; their
+// verdicts replace the UNDECIDED placeholder.  Messages the host decoder cannot
+// express (more than MOCHI_MAX_OPS_PER_CERT operations, a grant over 64 KiB,
+// op_flags_off disagreeing with the operation count) stay UNDECIDED.
+static int decide_fallback(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
+                           const std::vector<uint32_t>& msgs) {
+  const uint32_t* ofo = w->op_flags_off;
+  std::vector<uint32_t> take;
+  std::vector<mochi_host::Message> dec;
+  for (uint32_t m : msgs) {
+    mochi_host::Message d;
+    if (mochi_host::decode_full(w->wire + w->msg_off[m], w->msg_len[m], c->server_ids, d) != MOCHI_MSG_OK) continue;
+    if (ofo && ofo[m + 1] - ofo[m] != d.ops.size()) continue;
+    bool fits = true;
+    for (auto& mg : d.mgs)
+      for (auto& g : mg.grants) fits &= g.bytes.size() <= 65536;
+    if (!fits) continue;
+    take.push_back(m);
+    dec.push_back(std::move(d));
+  }
+  if (take.empty()) return MOCHI_OK;
+  std::vector<uint8_t> blob, sig, gkey, opk, opf, hashes;
+  std::vector<uint64_t> goff, okoff;
+  std::vector<uint32_t> glen, cgo{0}, coo{0}, cmo{0}, mgo{0}, oklen;
+  std::vector<uint16_t> signer;
+  std::vector<int64_t> ots;
+  for (size_t i = 0; i < take.size(); i++) {
+    const uint32_t m = take[i];
+    const mochi_host::Message& d = dec[i];
+    for (auto& mg : d.mgs) {
+      for (auto& g : mg.grants) {
+        goff.push_back(blob.size());
+        glen.push_back((uint32_t)g.bytes.size());
+        blob.insert(blob.end(), g.bytes.begin(), g.bytes.end());
+        sig.insert(sig.end(), g.sig, g.sig + MOCHI_RSA_BYTES);
+        signer.push_back(mg.signer);
+        gkey.push_back(g.slot);
+      }
+      mgo.push_back((uint32_t)goff.size());
+    }
+    cmo.push_back((uint32_t)mgo.size() - 1);
+    cgo.push_back((uint32_t)goff.size());
+    for (size_t j = 0; j < d.ops.size(); j++) {
+      const auto& op = d.ops[j];
+      opk.push_back(op.slot);
+      const uint8_t fl = ofo ? w->op_flags[ofo[m] + j] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
+      opf.push_back((uint8_t)(fl | (op.not_write ? MOCHI_OP_NOT_WRITE : 0)));
+      ots.push_back(ofo && w->op_object_ts ? w->op_object_ts[ofo[m] + j] : 0);
+      okoff.push_back(blob.size());
+      oklen.push_back((uint32_t)op.key_bytes.size());
+      blob.insert(blob.end(), op.key_bytes.begin(), op.key_bytes.end());
+    }
+    coo.push_back((uint32_t)opk.size());
+    hashes.insert(hashes.end(), w->expected_hash + (size_t)m * MOCHI_TXN_HASH_BYTES,
+                  w->expected_hash + (size_t)(m + 1) * MOCHI_TXN_HASH_BYTES);
+  }
+  if (blob.empty()) blob.push_back(0);
+  mochi_batch b;
+  memset(&b, 0, sizeof b);
+  b.n_grants = (uint32_t)goff.size();
+  b.n_certs = (uint32_t)take.size();
+  b.n_ops = (uint32_t)opk.size();
+  b.n_mgs = (uint32_t)mgo.size() - 1;
+  b.grant_bytes_len = blob.size();
+  b.grant_bytes = blob.data();
+  b.grant_off = goff.data();
+  b.grant_len = glen.data();
+  b.sig = sig.data();
+  b.signer = signer.data();
+  b.grant_key = gkey.data();
+  b.cert_grant_off = cgo.data();
+  b.cert_op_off = coo.data();
+  b.op_key = opk.data();
+  b.op_flags = opf.data();
+  b.expected_hash = hashes.data();
+  b.cert_mg_off = cmo.data();
+  b.mg_grant_off = mgo.data();
+  b.op_object_ts = ots.data();
+  b.op_key_off = okoff.data();
+  b.op_key_len = oklen.data();
+  const size_t C = take.size(), O = opk.size();
+  std::vector<uint32_t> acc((C + 31) / 32), og0(O + 1);
+  std::vector<uint8_t> reason(C), fail(C), odec(O + 1);
+  std::vector<int64_t> ots_out(O + 1);
+  mochi_verdicts v;
+  memset(&v, 0, sizeof v);
+  v.cert_accept_bits = acc.data();
+  v.cert_reason = reason.data();
+  v.cert_fail_op = fail.data();
+  v.op_decision = odec.data();
+  v.op_g0 = og0.data();
+  v.op_ts = ots_out.data();
+  float saved[4] = {c->last_ms[0], c->last_ms[1], c->last_ms[2], c->last_total_ms};
+  const int rc = run_host_pipeline(c, &b, p, &v);
+  c->last_ms[0] = saved[0], c->last_ms[1] = saved[1], c->last_ms[2] = saved[2], c->last_total_ms = saved[3];
+  if (rc) return rc;
+  for (size_t i = 0; i < C; i++) {
+    const uint32_t m = take[i];
+    const bool a = (acc[i >> 5] >> (i & 31)) & 1u;
+    if (a) o->cert_accept_bits[m >> 5] |= 1u << (m & 31);
+    else o->cert_accept_bits[m >> 5] &= ~(1u << (m & 31));
+    if (o->cert_reason) o->cert_reason[m] = reason[i];
+    if (o->cert_fail_op) o->cert_fail_op[m] = fail[i];
+    if (ofo)
+      for (uint32_t j = 0; j < coo[i + 1] - coo[i]; j++) {
+        const size_t src = coo[i] + j, dst = ofo[m] + j;
+        if (o->op_decision) o->op_decision[dst] = odec[src];
+        if (o->op_g0) o->op_g0[dst] = og0[src];
+        if (o->op_ts) o->op_ts[dst] = ots_out[src];
+      }
+  }
+  return MOCHI_OK;
 }
 
 // ---- Write2 wire path, host memory: chunked pipeline -------------------------
@@ -1258,6 +1383,9 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);
   (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);
   (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
+  std::vector<uint32_t> fallback;
+  for (uint32_t m = 0; m < M; m++)
+    if (pout[o_status + m] == MOCHI_MSG_FALLBACK) fallback.push_back(m);
   memcpy(o->cert_accept_bits, pout + o_acc, nbits);
   if (o->cert_reason) memcpy(o->cert_reason, pout + o_reason, M);
   if (o->cert_fail_op) memcpy(o->cert_fail_op, pout + o_fail, M);
@@ -1265,6 +1393,7 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   if (o->op_decision) memcpy(o->op_decision, pout + o_dec, O_in);
   if (o->op_g0) memcpy(o->op_g0, pout + o_g0, 4 * O_in);
   if (o->op_ts) memcpy(o->op_ts, pout + o_ots, 8 * O_in);
+  if (!fallback.empty()) return decide_fallback(c, w, p, o, fallback);
   return MOCHI_OK;
 }
 

@@ -1305,7 +1305,428 @@ void oracle_w2_free(oracle_w2_decoded* d) {
   free((void*)d->batch.op_key_off);
   free((void*)d->batch.op_key_len);
   free(d->msg_status);
+  free(d->own_blob);
   memset(d, 0, sizeof *d);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Full Write2ToServer decode (the messages the device fast path declines),   */
+/* restated literally: a singular message field given several times is        */
+/* parsed as the CONCATENATION of its occurrences (protobuf merge semantics); */
+/* map entries: LinkedHashMap put (first position, last entry's value, whose  */
+/* message value is again the concatenation of its occurrences; a bytes value */
+/* takes the last occurrence).  The signed grant bytes are Grant.toByteArray()*/
+/* of the parsed Grant (MochiProtocol.java:7556-7574): known fields, then the */
+/* retained unknown fields (parseUnknownFieldProto3) as UnknownFieldSet       */
+/* writes them -- ascending field number; per number varint, fixed32,        */
+/* fixed64, length-delimited, group values in arrival order; group bodies     */
+/* normalised the same way.                                                    */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+  uint8_t* b;
+  size_t n, cap;
+} buf_t;
+
+static void buf_put(buf_t* o, const void* p, size_t n) {
+  if (o->n + n > o->cap) {
+    o->cap = (o->n + n) * 2 + 64;
+    o->b = (uint8_t*)realloc(o->b, o->cap);
+  }
+  memcpy(o->b + o->n, p, n);
+  o->n += n;
+}
+static void buf_varint(buf_t* o, uint64_t v) {
+  uint8_t t[10];
+  buf_put(o, t, put_varint(t, v));
+}
+
+/* concatenation of every wt-2 payload of field `field` in [off, off+len) */
+static void concat_field(const uint8_t* m, size_t off, size_t len, uint32_t field, buf_t* out) {
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc)
+    if (f.field == field && f.wt == 2) buf_put(out, m + off + f.off, f.len);
+}
+
+typedef struct {
+  uint32_t field;
+  int cls; /* 0 varint, 1 fixed32, 2 fixed64, 3 length-delimited, 4 group */
+  uint64_t v;
+  const uint8_t* p;
+  size_t n;
+} unk_t;
+
+/* Grant parse retaining unknown fields; returns 0 on malformed input. */
+typedef struct {
+  const uint8_t *oid, *hash;
+  size_t oid_n, hash_n;
+  int64_t ts, cfg;
+  int32_t status;
+  unk_t* unk;
+  size_t n_unk;
+} full_grant_t;
+
+static int collect_unknown(rd_t* r, uint32_t field, uint32_t wt, unk_t** list, size_t* n, int depth);
+
+/* body of a group that started before r->pos: returns its end offset (before the END tag) */
+static int group_body(rd_t* r, uint32_t field, size_t* body_end, int depth) {
+  if (depth > 100) return 0;
+  for (;;) {
+    const size_t at = r->pos;
+    uint64_t t64, v;
+    if (!rd_varint(r, &t64)) return 0;
+    const uint32_t t = (uint32_t)t64, f = t >> 3, wt = t & 7;
+    if (f == 0) return 0;
+    switch (wt) {
+      case 0: if (!rd_varint(r, &v)) return 0; break;
+      case 1: if (r->len - r->pos < 8) return 0; r->pos += 8; break;
+      case 2: {
+        if (!rd_varint(r, &v)) return 0;
+        const int32_t l = (int32_t)(uint32_t)v;
+        if (l < 0 || (uint64_t)l > r->len - r->pos) return 0;
+        r->pos += (size_t)l;
+        break;
+      }
+      case 3: { size_t e; if (!group_body(r, f, &e, depth + 1)) return 0; break; }
+      case 4: if (f != field) return 0; *body_end = at; return 1;
+      case 5: if (r->len - r->pos < 4) return 0; r->pos += 4; break;
+      default: return 0;
+    }
+  }
+}
+
+static int collect_unknown(rd_t* r, uint32_t field, uint32_t wt, unk_t** list, size_t* n, int depth) {
+  unk_t u;
+  memset(&u, 0, sizeof u);
+  u.field = field;
+  uint64_t v;
+  switch (wt) {
+    case 0: if (!rd_varint(r, &v)) return 0; u.cls = 0; u.v = v; break;
+    case 5: if (r->len - r->pos < 4) return 0; u.cls = 1; u.p = r->b + r->pos; u.n = 4; r->pos += 4; break;
+    case 1: if (r->len - r->pos < 8) return 0; u.cls = 2; u.p = r->b + r->pos; u.n = 8; r->pos += 8; break;
+    case 2: {
+      if (!rd_varint(r, &v)) return 0;
+      const int32_t l = (int32_t)(uint32_t)v;
+      if (l < 0 || (uint64_t)l > r->len - r->pos) return 0;
+      u.cls = 3; u.p = r->b + r->pos; u.n = (size_t)l; r->pos += (size_t)l;
+      break;
+    }
+    case 3: {
+      const size_t start = r->pos;
+      size_t end;
+      if (!group_body(r, field, &end, depth + 1)) return 0;
+      u.cls = 4; u.p = r->b + start; u.n = end - start;
+      break;
+    }
+    default: return 0;
+  }
+  *list = (unk_t*)realloc(*list, (*n + 1) * sizeof(unk_t));
+  (*list)[(*n)++] = u;
+  return 1;
+}
+
+/* UnknownFieldSet.writeTo of a list (arrival order): by field number, then class */
+static void write_unknowns(buf_t* o, const unk_t* u, size_t n);
+
+static void write_group_body(buf_t* o, const uint8_t* p, size_t n) {
+  rd_t r = {p, n, 0};
+  unk_t* list = NULL;
+  size_t k = 0;
+  while (r.pos < r.len) {
+    uint64_t t64;
+    if (!rd_varint(&r, &t64)) break;
+    const uint32_t t = (uint32_t)t64;
+    if (!collect_unknown(&r, t >> 3, t & 7, &list, &k, 1)) break;
+  }
+  write_unknowns(o, list, k);
+  free(list);
+}
+
+static void write_unknowns(buf_t* o, const unk_t* u, size_t n) {
+  /* selection over (field, class) pairs in ascending order, arrival order within */
+  uint64_t last = 0;
+  int first = 1;
+  for (;;) {
+    uint64_t best = UINT64_MAX;
+    for (size_t i = 0; i < n; i++) {
+      const uint64_t key = (uint64_t)u[i].field << 3 | (uint64_t)u[i].cls;
+      if ((first || key > last) && key < best) best = key;
+    }
+    if (best == UINT64_MAX) return;
+    for (size_t i = 0; i < n; i++) {
+      const uint64_t key = (uint64_t)u[i].field << 3 | (uint64_t)u[i].cls;
+      if (key != best) continue;
+      static const int wt_of[5] = {0, 5, 1, 2, 3};
+      buf_varint(o, (uint64_t)u[i].field << 3 | (uint64_t)wt_of[u[i].cls]);
+      switch (u[i].cls) {
+        case 0: buf_varint(o, u[i].v); break;
+        case 1: case 2: buf_put(o, u[i].p, u[i].n); break;
+        case 3: buf_varint(o, u[i].n); buf_put(o, u[i].p, u[i].n); break;
+        default:
+          write_group_body(o, u[i].p, u[i].n);
+          buf_varint(o, (uint64_t)u[i].field << 3 | 4);
+      }
+    }
+    last = best;
+    first = 0;
+  }
+}
+
+static int parse_grant_full(const uint8_t* b, size_t n, full_grant_t* g) {
+  memset(g, 0, sizeof *g);
+  rd_t r = {b, n, 0};
+  while (r.pos < r.len) {
+    uint64_t t64, v;
+    if (!rd_varint(&r, &t64)) return 0;
+    const uint32_t tag = (uint32_t)t64, field = tag >> 3, wt = tag & 7;
+    if (field == 0) return 0;
+    uint32_t so, sl;
+    switch (tag) {
+      case 10: if (!rd_string(&r, &so, &sl)) return 0; g->oid = b + so; g->oid_n = sl; continue;
+      case 16: if (!rd_varint(&r, &v)) return 0; g->ts = (int64_t)v; continue;
+      case 24: if (!rd_varint(&r, &v)) return 0; g->cfg = (int64_t)v; continue;
+      case 34: if (!rd_string(&r, &so, &sl)) return 0; g->hash = b + so; g->hash_n = sl; continue;
+      case 40: if (!rd_varint(&r, &v)) return 0; g->status = (int32_t)(uint32_t)v; continue;
+      default:
+        if (wt == 4) return 0;
+        if (!collect_unknown(&r, field, wt, &g->unk, &g->n_unk, 0)) return 0;
+    }
+  }
+  return 1;
+}
+
+static void grant_to_bytes(const full_grant_t* g, buf_t* o) {
+  uint8_t tmp[1];
+  (void)tmp;
+  if (g->oid_n) { buf_varint(o, 10); buf_varint(o, g->oid_n); buf_put(o, g->oid, g->oid_n); }
+  if (g->ts) { buf_varint(o, 16); buf_varint(o, (uint64_t)g->ts); }
+  if (g->cfg) { buf_varint(o, 24); buf_varint(o, (uint64_t)g->cfg); }
+  if (g->hash_n) { buf_varint(o, 34); buf_varint(o, g->hash_n); buf_put(o, g->hash, g->hash_n); }
+  if (g->status) { buf_varint(o, 40); buf_varint(o, (uint64_t)(int64_t)g->status); }
+  write_unknowns(o, g->unk, g->n_unk);
+}
+
+/* map entries of field `field` in [off, off+len): key (last) and the concatenation
+ * of the value occurrences (last occurrence only when last_only) */
+typedef struct {
+  const uint8_t* k;
+  size_t kn;
+  buf_t val;
+} fentry_t;
+
+static size_t full_entries(const uint8_t* m, size_t off, size_t len, uint32_t field, int last_only, fentry_t** out) {
+  fentry_t* v = NULL;
+  size_t n = 0;
+  fld_t f;
+  int rc;
+  FOR_FIELDS(m, off, len, f, rc) {
+    if (f.field != field || f.wt != 2) continue;
+    v = (fentry_t*)realloc(v, (n + 1) * sizeof *v);
+    fentry_t* e = &v[n++];
+    memset(e, 0, sizeof *e);
+    fld_t g;
+    int rc2;
+    const size_t eo = off + f.off;
+    FOR_FIELDS(m, eo, f.len, g, rc2) {
+      if (g.wt != 2) continue;
+      if (g.field == 1) { e->k = m + eo + g.off; e->kn = g.len; }
+      if (g.field == 2) {
+        if (last_only) e->val.n = 0;
+        buf_put(&e->val, m + eo + g.off, g.len);
+      }
+    }
+  }
+  *out = v;
+  return n;
+}
+
+static void free_entries(fentry_t* e, size_t n) {
+  for (size_t i = 0; i < n; i++) free(e[i].val.b);
+  free(e);
+}
+
+/* index of the entry holding the final value of e[i]'s key, or -1 if e[i] is not the key's first entry */
+static long fmap_slot(const fentry_t* e, size_t n, size_t i) {
+  for (size_t j = 0; j < i; j++)
+    if (e[j].kn == e[i].kn && (e[i].kn == 0 || memcmp(e[j].k, e[i].k, e[i].kn) == 0)) return -1;
+  size_t last = i;
+  for (size_t j = i + 1; j < n; j++)
+    if (e[j].kn == e[i].kn && (e[i].kn == 0 || memcmp(e[j].k, e[i].k, e[i].kn) == 0)) last = j;
+  return (long)last;
+}
+
+/* index of the last entry whose key equals k, -1 if none (map value of key k) */
+static long fmap_slot_key(const fentry_t* e, size_t n, const uint8_t* k, size_t kn) {
+  long last = -1;
+  for (size_t j = 0; j < n; j++)
+    if (e[j].kn == kn && (kn == 0 || memcmp(e[j].k, k, kn) == 0)) last = (long)j;
+  return last;
+}
+
+/* Decode message m fully into `b` (appending one certificate): grants,
+ * MultiGrants, ops; grant and op-key bytes go to `blob`.  Returns
+ * MOCHI_MSG_OK, or MOCHI_MSG_FALLBACK when it has more than
+ * MOCHI_MAX_OPS_PER_CERT operations (one-byte op slots). */
+typedef struct {
+  buf_t blob;
+  gout_t go;
+  mgout_t mg;
+  uint8_t* opk;
+  uint8_t* opn; /* MOCHI_OP_NOT_WRITE per op */
+  uint64_t* oko;
+  uint32_t* okl;
+  size_t on;
+} full_out_t;
+
+static int decode_full_one(const uint8_t* m, size_t mlen, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids,
+                           full_out_t* o) {
+  buf_t wc = {0}, tx = {0};
+  concat_field(m, 0, mlen, 1, &wc);
+  concat_field(m, 0, mlen, 2, &tx);
+  int status = MOCHI_MSG_OK;
+  /* operations: every field-1 occurrence of the transaction is one Operation */
+  size_t op_o[1024], op_l[1024];
+  size_t no = 0;
+  uint8_t slots[1024];
+  fld_t f;
+  int rc;
+  const size_t on0 = o->on;
+  if (wc.n == 0 && wc.b == NULL) wc.b = (uint8_t*)malloc(1);
+  if (tx.b == NULL) tx.b = (uint8_t*)malloc(1);
+  FOR_FIELDS(tx.b, 0, tx.n, f, rc) {
+    if (f.field != 1 || f.wt != 2) continue;
+    if (no == 1024) { status = MOCHI_MSG_FALLBACK; break; }
+    last_string(tx.b, f.off, f.len, 2, &op_o[no], &op_l[no]);
+    const int32_t action = (int32_t)(uint32_t)last_varint(tx.b, f.off, f.len, 1);
+    uint32_t slot = (uint32_t)no;
+    for (size_t j = 0; j < no; j++)
+      if (same(tx.b, op_o[j], op_l[j], op_o[no], op_l[no])) { slot = slots[j]; break; }
+    slots[no] = (uint8_t)(slot < 255 ? slot : 255);
+    o->opk = (uint8_t*)realloc(o->opk, o->on + 1);
+    o->opn = (uint8_t*)realloc(o->opn, o->on + 1);
+    o->oko = (uint64_t*)realloc(o->oko, (o->on + 1) * sizeof(uint64_t));
+    o->okl = (uint32_t*)realloc(o->okl, (o->on + 1) * sizeof(uint32_t));
+    o->opk[o->on] = slots[no];
+    o->opn[o->on] = (action != 1 && action != 2) || op_l[no] == 0 ? MOCHI_OP_NOT_WRITE : 0;
+    o->oko[o->on] = o->blob.n;
+    o->okl[o->on] = (uint32_t)op_l[no];
+    buf_put(&o->blob, tx.b + op_o[no], op_l[no]);
+    o->on++;
+    no++;
+  }
+  if (no > MOCHI_MAX_OPS_PER_CERT) status = MOCHI_MSG_FALLBACK;
+  const uint32_t g0 = o->go.n, m0 = o->mg.n;
+  if (status == MOCHI_MSG_OK) {
+    fentry_t* ce;
+    const size_t nce = full_entries(wc.b, 0, wc.n, 1, 0, &ce);
+    for (size_t i = 0; i < nce; i++) {
+      const long s = fmap_slot(ce, nce, i);
+      if (s < 0) continue;
+      const fentry_t* mgv = &ce[s];
+      const uint8_t* mb = mgv->val.b ? mgv->val.b : (const uint8_t*)"";
+      size_t sid_o, sid_l;
+      last_string(mb, 0, mgv->val.n, 4, &sid_o, &sid_l);
+      uint16_t signer = 0xFFFF;
+      for (uint32_t k = 0; k < n_ids; k++)
+        if (id_off[k + 1] - id_off[k] == sid_l && memcmp(ids + id_off[k], mb + sid_o, sid_l) == 0) { signer = (uint16_t)k; break; }
+      fentry_t *ge, *se;
+      const size_t nge = full_entries(mb, 0, mgv->val.n, 1, 0, &ge);
+      const size_t nse = full_entries(mb, 0, mgv->val.n, 5, 1, &se);
+      uint32_t n_g = 0;
+      for (size_t a = 0; a < nge; a++) {
+        const long t = fmap_slot(ge, nge, a);
+        if (t < 0) continue;
+        full_grant_t g;
+        if (!parse_grant_full(ge[t].val.b ? ge[t].val.b : (const uint8_t*)"", ge[t].val.n, &g)) { status = MOCHI_MSG_MALFORMED; free(g.unk); break; }
+        const uint64_t goff = o->blob.n;
+        grant_to_bytes(&g, &o->blob);
+        free(g.unk);
+        const uint8_t* sig = NULL;
+        const long st = fmap_slot_key(se, nse, ge[a].k, ge[a].kn);
+        if (st >= 0 && se[st].val.n == MOCHI_RSA_BYTES) sig = se[st].val.b;
+        uint8_t key = 0xFF;
+        for (size_t j = 0; j < no; j++)
+          if (op_l[j] == ge[a].kn && (ge[a].kn == 0 || memcmp(tx.b + op_o[j], ge[a].k, ge[a].kn) == 0)) { key = slots[j]; break; }
+        gout_push(&o->go, goff, (uint32_t)(o->blob.n - goff), sig, signer, key);
+        n_g++;
+      }
+      mg_push(&o->mg, n_g);
+      free_entries(ge, nge);
+      free_entries(se, nse);
+      if (status != MOCHI_MSG_OK) break;
+    }
+    free_entries(ce, nce);
+  }
+  if (status != MOCHI_MSG_OK) {
+    o->go.n = g0;
+    o->mg.n = m0;
+    o->on = on0;
+  }
+  free(wc.b);
+  free(tx.b);
+  return status;
+}
+
+int oracle_w2_decode_full(const mochi_write2_batch* w, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids,
+                          oracle_w2_decoded* out) {
+  if (!w || !out) return MOCHI_EINVAL;
+  memset(out, 0, sizeof *out);
+  const uint32_t M = w->n_msgs;
+  full_out_t o;
+  memset(&o, 0, sizeof o);
+  uint32_t* cg = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
+  uint32_t* co = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
+  uint32_t* cm = (uint32_t*)calloc(M + 1, sizeof(uint32_t));
+  uint8_t* st = (uint8_t*)calloc(M ? M : 1, 1);
+  for (uint32_t i = 0; i < M; i++) {
+    const uint8_t* m = w->wire + w->msg_off[i];
+    const size_t ml = w->msg_len[i];
+    st[i] = (uint8_t)(valid_write2(m, ml) ? decode_full_one(m, ml, ids, id_off, n_ids, &o) : MOCHI_MSG_MALFORMED);
+    cg[i + 1] = o.go.n;
+    co[i + 1] = (uint32_t)o.on;
+    cm[i + 1] = o.mg.n;
+  }
+  uint32_t* mgo = (uint32_t*)malloc(((size_t)o.mg.n + 1) * sizeof(uint32_t));
+  mgo[0] = 0;
+  for (uint32_t j = 0; j < o.mg.n; j++) mgo[j + 1] = mgo[j] + o.mg.cnt[j];
+  free(o.mg.cnt);
+  if (!o.blob.b) o.blob.b = (uint8_t*)malloc(1);
+  uint8_t* opf = (uint8_t*)malloc(o.on + 1);
+  int64_t* opt = (int64_t*)calloc(o.on + 1, sizeof(int64_t));
+  for (uint32_t i = 0; i < M; i++)
+    for (uint32_t j = co[i]; j < co[i + 1]; j++) {
+      const int flagged = w->op_flags_off && w->op_flags_off[i + 1] - w->op_flags_off[i] == co[i + 1] - co[i];
+      opf[j] = (uint8_t)((flagged ? w->op_flags[w->op_flags_off[i] + j - co[i]] : (MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC)) |
+                         o.opn[j]);
+      opt[j] = flagged && w->op_object_ts ? w->op_object_ts[w->op_flags_off[i] + j - co[i]] : 0;
+    }
+  free(o.opn);
+  mochi_batch* b = &out->batch;
+  b->n_grants = o.go.n;
+  b->n_certs = M;
+  b->n_ops = (uint32_t)o.on;
+  b->n_mgs = cm[M];
+  b->grant_bytes_len = o.blob.n;
+  b->grant_bytes = o.blob.b;
+  b->grant_off = o.go.off;
+  b->grant_len = o.go.len;
+  b->sig = o.go.sig;
+  b->signer = o.go.signer;
+  b->grant_key = o.go.key;
+  b->cert_grant_off = cg;
+  b->cert_op_off = co;
+  b->op_key = o.opk ? o.opk : (uint8_t*)malloc(1);
+  b->op_flags = opf;
+  b->expected_hash = w->expected_hash;
+  b->cert_mg_off = cm;
+  b->mg_grant_off = mgo;
+  b->op_object_ts = opt;
+  b->op_key_off = o.oko;
+  b->op_key_len = o.okl;
+  out->msg_status = st;
+  out->own_blob = o.blob.b;
+  return MOCHI_OK;
 }
 
 int oracle_verify_write2(const uint8_t* moduli_be, uint32_t n_keys, const uint8_t* ids, const uint32_t* id_off,
@@ -1349,6 +1770,55 @@ int oracle_verify_write2(const uint8_t* moduli_be, uint32_t n_keys, const uint8_
   free(v.op_decision);
   free(v.op_g0);
   free(v.op_ts);
+  /* FALLBACK messages: the full decode, verified like any other certificate.
+   * Left UNDECIDED: more than MOCHI_MAX_OPS_PER_CERT operations, op_flags_off
+   * disagreeing with the operation count, or a grant over 64 KiB. */
+  uint32_t n_fb = 0;
+  for (uint32_t i = 0; rc == MOCHI_OK && i < w->n_msgs; i++) n_fb += d.msg_status[i] == MOCHI_MSG_FALLBACK;
+  if (rc == MOCHI_OK && n_fb) {
+    oracle_w2_decoded f;
+    rc = oracle_w2_decode_full(w, ids, id_off, n_keys, &f);
+    if (rc == MOCHI_OK) {
+      const uint32_t C = w->n_msgs, O = f.batch.n_ops, N = f.batch.n_grants;
+      mochi_verdicts fv;
+      memset(&fv, 0, sizeof fv);
+      fv.cert_accept_bits = (uint32_t*)calloc((C + 31) / 32 + 1, 4);
+      fv.cert_reason = (uint8_t*)malloc(C + 1);
+      fv.cert_fail_op = (uint8_t*)malloc(C + 1);
+      fv.op_decision = (uint8_t*)malloc(O + 1);
+      fv.op_g0 = (uint32_t*)malloc(4 * ((size_t)O + 1));
+      fv.op_ts = (int64_t*)malloc(8 * ((size_t)O + 1));
+      rc = oracle_verify_batch(moduli_be, n_keys, &f.batch, p, &fv, n_threads);
+      for (uint32_t i = 0; rc == MOCHI_OK && i < C; i++) {
+        if (d.msg_status[i] != MOCHI_MSG_FALLBACK || f.msg_status[i] != MOCHI_MSG_OK) continue;
+        const uint32_t lo = f.batch.cert_op_off[i], no = f.batch.cert_op_off[i + 1] - lo;
+        if (w->op_flags_off && w->op_flags_off[i + 1] - w->op_flags_off[i] != no) continue;
+        int big = 0;
+        for (uint32_t g = f.batch.cert_grant_off[i]; g < f.batch.cert_grant_off[i + 1]; g++) big |= f.batch.grant_len[g] > 65536;
+        if (big) continue;
+        const int a = (fv.cert_accept_bits[i >> 5] >> (i & 31)) & 1;
+        if (a) out->cert_accept_bits[i >> 5] |= 1u << (i & 31);
+        else out->cert_accept_bits[i >> 5] &= ~(1u << (i & 31));
+        if (out->cert_reason) out->cert_reason[i] = fv.cert_reason[i];
+        if (out->cert_fail_op) out->cert_fail_op[i] = fv.cert_fail_op[i];
+        if (per_op)
+          for (uint32_t j = 0; j < no; j++) {
+            const size_t dst = w->op_flags_off[i] + j;
+            if (out->op_decision) out->op_decision[dst] = fv.op_decision[lo + j];
+            if (out->op_g0) out->op_g0[dst] = fv.op_g0[lo + j];
+            if (out->op_ts) out->op_ts[dst] = fv.op_ts[lo + j];
+          }
+      }
+      (void)N;
+      free(fv.cert_accept_bits);
+      free(fv.cert_reason);
+      free(fv.cert_fail_op);
+      free(fv.op_decision);
+      free(fv.op_g0);
+      free(fv.op_ts);
+      oracle_w2_free(&f);
+    }
+  }
   oracle_w2_free(&d);
   return rc;
 }

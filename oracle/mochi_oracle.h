@@ -112,13 +112,24 @@ int oracle_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const 
 typedef struct oracle_w2_decoded {
   mochi_batch batch;
   uint8_t* msg_status; /* [M] enum mochi_msg_status */
+  uint8_t* own_blob;   /* oracle_w2_decode_full: the blob batch.grant_bytes points into */
 } oracle_w2_decoded;
 int oracle_w2_decode(const mochi_write2_batch* w, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids,
                      oracle_w2_decoded* out);
 void oracle_w2_free(oracle_w2_decoded* d);
 
-/* Decode + oracle_verify_batch + the per-message status fix-up; same contract
- * as mochi_verify_write2. */
+/* Full protobuf-java decode of every message (no fast-path limits: merged
+ * repeated fields, merged map values, non-canonical Grant bytes re-serialized
+ * as Grant.toByteArray() incl. retained unknown fields, any number of
+ * MultiGrants / grants).  grant_bytes is a new blob (own_blob) of the signed
+ * bytes; op keys are slices of it.  msg_status: OK, MALFORMED, or FALLBACK for
+ * more than MOCHI_MAX_OPS_PER_CERT operations. */
+int oracle_w2_decode_full(const mochi_write2_batch* w, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids,
+                          oracle_w2_decoded* out);
+
+/* Decode + oracle_verify_batch + the per-message status fix-up; FALLBACK
+ * messages are decided through oracle_w2_decode_full.  Same contract as
+ * mochi_verify_write2. */
 int oracle_verify_write2(const uint8_t* moduli_be, uint32_t n_keys, const uint8_t* ids, const uint32_t* id_off,
                          const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* out, uint8_t* msg_status,
                          int n_threads);

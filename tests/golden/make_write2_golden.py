@@ -129,8 +129,12 @@ def vectors():
     base_ops = [op(A), op(B)]
     V = []
 
-    def add(name, data, status, order=None, why=""):
-        V.append(dict(name=name, hex=data.hex(), status=status, order=order, why=why))
+    def add(name, data, status, order=None, why="", full=None, full_status=0):
+        # full / full_status: for fast-path exits (status 2), the order the library's host decoder
+        # (full protobuf-java semantics) must produce, and whether it decides the message (0) or
+        # leaves it undecided (2: more than 64 operations)
+        V.append(dict(name=name, hex=data.hex(), status=status, order=order, why=why,
+                      full=full if status == 2 else order, full_status=full_status if status == 2 else status))
 
     order3 = {"certs": [SID[0], SID[1], SID[2]], "grants": [[A, B]] * 3, "ops": [A, B]}
     add("canonical", w2(base_mgs, base_ops), 0, order3)
@@ -178,13 +182,31 @@ def vectors():
     # fast-path exits (legal protobuf, host fallback)
     wc_bytes = b"".join(ent(1, k.encode(), v) for k, v in base_mgs)
     tx_bytes = b"".join(ld(1, o) for o in base_ops)
-    add("write_certificate_twice", ld(1, wc_bytes[:len(wc_bytes) // 2] if False else wc_bytes) + ld(2, tx_bytes) + ld(1, b""), 2,
-        why="singular message field repeated: protobuf merges, fast path declines")
-    add("transaction_twice", ld(1, wc_bytes) + ld(2, tx_bytes) + ld(2, ld(1, op("C"))), 2)
+    add("write_certificate_twice", ld(1, wc_bytes) + ld(2, tx_bytes) + ld(1, b""), 2,
+        why="singular message field repeated: protobuf merges, fast path declines", full=order3)
+    add("transaction_twice", ld(1, wc_bytes) + ld(2, tx_bytes) + ld(2, ld(1, op("C"))), 2,
+        full={"certs": [SID[0], SID[1], SID[2]], "grants": [[A, B]] * 3, "ops": [A, B, "C"]})
     mg_twice = ld(1, ld(1, SID[0].encode()) + ld(2, std(0)) + ld(2, W.encode_multigrant([], "", "", "", None)))
-    add("multigrant_value_twice", ld(1, mg_twice + b"".join(ent(1, k.encode(), v) for k, v in base_mgs[1:])) + ld(2, tx_bytes), 2)
+    add("multigrant_value_twice", ld(1, mg_twice + b"".join(ent(1, k.encode(), v) for k, v in base_mgs[1:])) + ld(2, tx_bytes), 2,
+        full=order3)
     g_twice = ld(1, ld(1, A.encode()) + ld(2, gA[0]) + ld(2, W.encode_grant("", 77, "")))
-    add("grant_value_twice", w2([(SID[0], g_twice + ld(4, SID[0].encode())), base_mgs[1], base_mgs[2]], base_ops), 2)
+    add("grant_value_twice", w2([(SID[0], g_twice + ld(4, SID[0].encode())), base_mgs[1], base_mgs[2]], base_ops), 2,
+        full={"certs": [SID[0], SID[1], SID[2]], "grants": [[A], [A, B], [A, B]], "ops": [A, B]})
+    # the same key's MultiGrant given in two certificate entries AND merged: last entry wins, no merge across entries
+    add("cert_key_twice_not_merged", w2([(SID[0], std(0)), (SID[0], mg(SID[0], [(B, gB[0])], [(B, sig(1))])),
+                                         base_mgs[1]], base_ops) + ld(1, ent(1, SID[2].encode(), std(2))), 2,
+        full={"certs": [SID[0], SID[1], SID[2]], "grants": [[B], [A, B], [A, B]], "ops": [A, B]})
+    # unknown fields of several numbers / wire types inside a Grant: Grant.toByteArray() re-emits them
+    # (UnknownFieldSet: ascending field number; per number varint, fixed32, fixed64, bytes, group)
+    unk_g = g(A, 5) + ld(9, b"zz") + var(7 << 3 | 5) + b"\x01\x02\x03\x04" + var(9 << 3 | 0) + var(3) + \
+        var(7 << 3 | 0) + var(8) + var(8 << 3 | 3) + var(2 << 3 | 0) + var(1) + var(8 << 3 | 4)
+    add("grant_unknown_fields_reordered", w2([(SID[0], mg(SID[0], [(A, unk_g)], [(A, sig(0))]))], [op(A)]), 2,
+        full={"certs": [SID[0]], "grants": [[A]], "ops": [A]},
+        why="Python's serializer keeps unknown fields in arrival order; protobuf-java's UnknownFieldSet sorts "
+            "them, so the Java bytes are written here by hand (java_grant_bytes)")
+    V[-1]["java_grant_bytes"] = {SID[0]: {A: (g(A, 5) + var(7 << 3 | 0) + var(8) + var(7 << 3 | 5) +
+                                              b"\x01\x02\x03\x04" + var(8 << 3 | 3) + var(2 << 3 | 0) + var(1) +
+                                              var(8 << 3 | 4) + var(9 << 3 | 0) + var(3) + ld(9, b"zz")).hex()}}
     noncanon = [
         ("grant_ts_explicit_zero", b"\x0a\x0a" + A.encode() + b"\x10\x00" + ld(4, th.encode())),
         ("grant_fields_out_of_order", ld(4, th.encode()) + b"\x0a\x0a" + A.encode() + b"\x10\x05"),
@@ -195,16 +217,20 @@ def vectors():
     ]
     for name, gb in noncanon:
         add(name, w2([(SID[0], mg(SID[0], [(A, gb)], [(A, sig(0))]))], [op(A)]), 2,
-            why="Grant bytes differ from Grant.toByteArray() of the parsed Grant")
+            why="Grant bytes differ from Grant.toByteArray() of the parsed Grant",
+            full={"certs": [SID[0]], "grants": [[A]], "ops": [A]})
     many = [(f"s{i}", mg(f"s{i}", [(A, gA[0])])) for i in range(33)]
-    add("33_multigrants", w2(many, [op(A)]), 2)
+    add("33_multigrants", w2(many, [op(A)]), 2, full={"certs": [f"s{i}" for i in range(33)], "grants": [[A]] * 33,
+                                                       "ops": [A]})
     add("32_multigrants", w2(many[:32], [op(A)]), 0,
         {"certs": [f"s{i}" for i in range(32)], "grants": [[A]] * 32, "ops": [A]})
-    add("65_operations", w2(base_mgs, [op(f"k{i}") for i in range(65)]), 2)
+    add("65_operations", w2(base_mgs, [op(f"k{i}") for i in range(65)]), 2, full_status=2,
+        why="op key slots are one byte (< 64): left undecided, never accepted")
     add("64_operations", w2(base_mgs, [op(f"k{i}") for i in range(64)]), 0,
         {"certs": [SID[0], SID[1], SID[2]], "grants": [[A, B]] * 3, "ops": [f"k{i}" for i in range(64)]})
     g65 = mg(SID[0], [(f"k{i}", g(f"k{i}", 3)) for i in range(65)])
-    add("65_grants_in_multigrant", w2([(SID[0], g65)], [op("k0")]), 2)
+    add("65_grants_in_multigrant", w2([(SID[0], g65)], [op("k0")]), 2,
+        full={"certs": [SID[0]], "grants": [[f"k{i}" for i in range(65)]], "ops": ["k0"]})
     # malformed (the protobuf parser throws)
     canon = w2(base_mgs, base_ops)
     for cut in (1, 2, 5, 40, len(canon) // 2, len(canon) - 1):

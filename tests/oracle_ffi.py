@@ -46,6 +46,7 @@ def lib():
         L.oracle_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_w2_decode.argtypes = [vp, vp, vp, u32, vp]
         L.oracle_w2_free.argtypes = [vp]
+        L.oracle_w2_decode_full.argtypes = [vp, vp, vp, u32, vp]
         L.oracle_verify_write2.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, ctypes.c_int]
         L.oracle_rsa_sign.argtypes = [ctypes.c_char_p, vp, sz, vp]
         L.oracle_pem_modulus.argtypes = [ctypes.c_char_p, vp]
@@ -234,20 +235,17 @@ def _w2_c(wb):
     return mh.write2_batch_c(wb)
 
 
-def w2_decode(wb, ids, id_off):
-    """Oracle decode of a workload.WireBatch -> dict of numpy arrays (grant_off,
-    grant_len, sig, signer, grant_key, cert_grant_off, cert_op_off, op_key,
-    op_flags, msg_status)."""
+def _dec_struct():
     import mochi_hip as mh
 
     class Dec(ctypes.Structure):
-        _fields_ = [("batch", mh.Batch_C), ("msg_status", ctypes.POINTER(ctypes.c_uint8))]
+        _fields_ = [("batch", mh.Batch_C), ("msg_status", ctypes.POINTER(ctypes.c_uint8)),
+                    ("own_blob", ctypes.c_void_p)]
 
-    wc, keep = _w2_c(wb)
-    d = Dec()
-    rc = lib().oracle_w2_decode(ctypes.addressof(wc), ids.ctypes.data, id_off.ctypes.data, int(id_off.shape[0]) - 1,
-                                ctypes.addressof(d))
-    assert rc == 0
+    return Dec
+
+
+def _dec_arrays(d, wire=None):
     b = d.batch
     N, C, O = b.n_grants, b.n_certs, b.n_ops
 
@@ -267,6 +265,34 @@ def w2_decode(wb, ids, id_off):
         cert_mg_off=arr(b.cert_mg_off, C + 1, np.uint32), mg_grant_off=arr(b.mg_grant_off, b.n_mgs + 1, np.uint32),
         op_key_off=arr(b.op_key_off, O, np.uint64), op_key_len=arr(b.op_key_len, O, np.uint32),
         op_object_ts=arr(b.op_object_ts, O, np.int64))
+    if d.own_blob:
+        out["blob"] = arr(d.own_blob, int(b.grant_bytes_len), np.uint8)
+    return out
+
+
+def w2_decode(wb, ids, id_off):
+    """Oracle decode of a workload.WireBatch (the device fast path's semantics) -> dict
+    of numpy arrays (grant_off, grant_len, sig, signer, grant_key, cert_grant_off,
+    cert_op_off, op_key, op_flags, msg_status, MultiGrant CSR, op key slices)."""
+    wc, keep = _w2_c(wb)
+    d = _dec_struct()()
+    rc = lib().oracle_w2_decode(ctypes.addressof(wc), ids.ctypes.data, id_off.ctypes.data, int(id_off.shape[0]) - 1,
+                                ctypes.addressof(d))
+    assert rc == 0
+    out = _dec_arrays(d)
+    lib().oracle_w2_free(ctypes.addressof(d))
+    return out
+
+
+def w2_decode_full(wb, ids, id_off):
+    """Oracle FULL decode (no fast-path limits); grant_off / op_key_off index out["blob"],
+    the re-serialized signed grant bytes."""
+    wc, keep = _w2_c(wb)
+    d = _dec_struct()()
+    rc = lib().oracle_w2_decode_full(ctypes.addressof(wc), ids.ctypes.data, id_off.ctypes.data,
+                                     int(id_off.shape[0]) - 1, ctypes.addressof(d))
+    assert rc == 0
+    out = _dec_arrays(d)
     lib().oracle_w2_free(ctypes.addressof(d))
     return out
 

@@ -72,12 +72,18 @@ def _single(data: bytes, n_ops=None):
                        expected_hash=np.zeros((1, 128), np.uint8))
 
 
-def check_decode_against_golden(v, d, wire, ids):
-    """Decoded arrays of one golden message vs its pinned status / order / content."""
-    assert int(d["msg_status"][0]) == v["status"], v["name"]
-    if v["status"] != 0:
+def check_decode_against_golden(v, d, wire, ids, full=False):
+    """Decoded arrays of one golden message vs its pinned status / order / content.
+    full=True: the full (host) decode -- v["full"] / v["full_status"], grant bytes in
+    d["blob"] (re-serialized Grant.toByteArray())."""
+    status, order = (v["full_status"], v["full"]) if full else (v["status"], v["order"])
+    assert int(d["msg_status"][0]) == status, v["name"]
+    if status != 0:
         return
-    order, content = v["order"], v["py_content"]
+    content = v["py_content"]
+    java = v.get("java_grant_bytes", {})
+    if full:
+        wire = d["blob"]
     assert [o for o in order["ops"]] == content["ops"], v["name"]
     # op slots: ops naming the same operand1 share a slot
     exp_slots = [order["ops"].index(k) for k in order["ops"]]
@@ -90,7 +96,7 @@ def check_decode_against_golden(v, d, wire, ids):
         notw = act not in (1, 2) or k == ""
         assert bool(d["op_flags"][j] & 0x10) == notw, (v["name"], j, act)
         o, n = int(d["op_key_off"][j]), int(d["op_key_len"][j])
-        assert wire[o:o + n].decode() == k, (v["name"], j)
+        assert bytes(wire[o:o + n]).decode() == k, (v["name"], j)
     # MultiGrant boundaries: one per certificate entry (first occurrence), its grants
     assert d["cert_mg_off"].tolist() == [0, len(order["certs"])], v["name"]
     assert np.diff(d["mg_grant_off"]).tolist() == [len(x) for x in order["grants"]], v["name"]
@@ -102,7 +108,8 @@ def check_decode_against_golden(v, d, wire, ids):
         exp_signer = ids.index(sid) if sid in ids else 0xFFFF
         for gkey in order["grants"][ci]:
             o, n = int(d["grant_off"][g]), int(d["grant_len"][g])
-            assert wire[o:o + n].hex() == c["grants"][gkey], (v["name"], ckey, gkey)
+            exp = java.get(ckey, {}).get(gkey, c["grants"][gkey])
+            assert bytes(wire[o:o + n]).hex() == exp, (v["name"], ckey, gkey)
             assert int(d["signer"][g]) == exp_signer, v["name"]
             s = c["sigs"].get(gkey)
             exp_sig = bytes.fromhex(s) if s is not None and len(s) == 512 else bytes(256)
@@ -122,6 +129,24 @@ def test_oracle_decode_matches_golden_vectors():
         data = bytes.fromhex(v["hex"])
         d = O.w2_decode(_single(data), blob, off)
         check_decode_against_golden(v, d, data, ids)
+
+
+def test_oracle_full_decode_matches_golden_vectors():
+    """The oracle's full protobuf-java decode (what the library's host decoder must
+    match for fast-path exits): merged repeated fields, merged map values, last-entry
+    map values, re-serialized Grant bytes (python google.protobuf pins the values;
+    protobuf-java's unknown-field order is written by hand), any MultiGrant count."""
+    vecs, ids, blob, off = _golden()
+    n_full = 0
+    for v in vecs:
+        data = bytes.fromhex(v["hex"])
+        d = O.w2_decode_full(_single(data), blob, off)
+        if v["status"] == 1:
+            assert int(d["msg_status"][0]) == 1, v["name"]
+            continue
+        check_decode_against_golden(v, d, data, ids, full=True)
+        n_full += v["status"] == 2 and v["full_status"] == 0
+    assert n_full >= 14
 
 
 def test_oracle_ops_mismatch_status():

@@ -286,3 +286,119 @@ def test_batcher_concurrent_callers(pool4, with_flags):
     np.testing.assert_array_equal(np.array([r[1] for r in res], np.uint8), ref.cert_reason)
     np.testing.assert_array_equal(np.array([r[3] for r in res], np.uint8), ref_st)
     ver.close()
+
+
+def _fields(b):
+    """(tag, raw field bytes) of a protobuf message with varint / length-delimited fields."""
+    out, i = [], 0
+    while i < len(b):
+        j = i
+        while b[j] & 0x80:
+            j += 1
+        tag = b[i]
+        j += 1
+        if tag & 7 == 0:
+            while b[j] & 0x80:
+                j += 1
+            j += 1
+        else:
+            n, sh, k = 0, 0, j
+            while True:
+                n |= (b[k] & 0x7F) << sh
+                sh += 7
+                k += 1
+                if not b[k - 1] & 0x80:
+                    break
+            j = k + n
+        out.append((tag, b[i:j]))
+        i = j
+    return out
+
+
+def _reorder(gb):
+    """A canonical Grant with its fields written in reverse order (same parsed Grant)."""
+    return b"".join(raw for _, raw in reversed(_fields(gb)))
+
+
+def _fallback_forms(s, c, ids):
+    """Certificate c of a synthetic batch re-encoded in legal forms the device fast path
+    declines (MOCHI_MSG_FALLBACK); the library's host decoder must decide them."""
+    b = s.batch
+    g0, g1 = int(b.cert_grant_off[c]), int(b.cert_grant_off[c + 1])
+    mgs = {}
+    for g in range(g0, g1):
+        gb = b.grant_bytes[int(b.grant_off[g]):int(b.grant_off[g]) + int(b.grant_len[g])].tobytes()
+        mgs.setdefault(int(b.signer[g]), []).append((W.grant_object_id(gb), gb, b.sig[g].tobytes()))
+    ent = [(ids[r], W.encode_multigrant([(o, gb) for o, gb, _ in it], ids[r], "cl", "", [(o, sg) for o, _, sg in it]))
+           for r, it in mgs.items()]
+    ops = [W.encode_operation(2, o) for o, _, _ in next(iter(mgs.values()))]
+    canon = W.encode_write2(ent, ops)
+    wc = b"".join(W.encode_map_entry(1, k.encode(), v) for k, v in ent)
+    tx = b"".join(W._ld(1, o) for o in ops)
+    oid, gb, _ = next(iter(mgs.values()))[0]
+    forms = {
+        "canonical": canon,
+        "wc_split": W._ld(1, wc[:len(W.encode_map_entry(1, ent[0][0].encode(), ent[0][1]))]) + W._ld(2, tx) +
+                    W._ld(1, wc[len(W.encode_map_entry(1, ent[0][0].encode(), ent[0][1])):]),
+        "tx_twice": W._ld(1, wc) + W._ld(2, tx) + W._ld(2, b""),
+        # 29 extra MultiGrants from unknown servers, unsigned, same grant: 33 MultiGrants in all
+        "33_multigrants": W.encode_write2(ent + [(f"extra-{i}", W.encode_multigrant([(oid, gb)], f"extra-{i}"))
+                                                 for i in range(29)], ops),
+        # every grant's fields out of canonical order: the signature covers the canonical
+        # re-encoding (Grant.toByteArray()), so it still verifies
+        "noncanonical_grants": W.encode_write2(
+            [(ids[r], W.encode_multigrant([(o, _reorder(gb)) for o, gb, _ in it], ids[r], "cl", "",
+                                          [(o, sg) for o, _, sg in it])) for r, it in mgs.items()], ops),
+    }
+    return forms
+
+
+def test_wire_fallback_messages_decided_on_host(pool4):
+    """Legal messages outside the device decoder's fast path are decoded on the host
+    with full protobuf-java semantics and verified on the device (signatures are never
+    skipped): same verdicts as their canonical form and as the oracle."""
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 64, first_cert=4242, faults=False)
+    ids4 = W.SERVER_IDS[:4]
+    msgs, kinds = [], []
+    for c in range(0, 64, 8):
+        for k, m in _fallback_forms(s, c, ids4).items():
+            msgs.append(m)
+            kinds.append(k)
+    wb = _pack(msgs, pad=1)
+    wb.expected_hash = np.stack([s.batch.expected_hash[c] for c in range(0, 64, 8) for _ in range(5)])
+    g, st = ver.verify_write2(wb, 4, True)
+    ids, off = W.server_id_table(4)
+    o, ost = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)
+    np.testing.assert_array_equal(st, ost)
+    np.testing.assert_array_equal(g.cert_reason, o.cert_reason)
+    np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits)
+    kinds = np.array(kinds)
+    assert (st[kinds == "canonical"] == mh.MSG_OK).all()
+    assert (st[(kinds == "wc_split") | (kinds == "tx_twice") | (kinds == "33_multigrants")] == mh.MSG_FALLBACK).all()
+    # decided, and like the canonical form: accepted (no faults in this stream)
+    assert g.cert_accept.all(), list(zip(kinds, g.cert_reason))
+    ver.close()
+
+
+def test_unsigned_33_multigrant_certificate_not_accepted(pool4):
+    """a client must not be able to skip signature checks by padding a
+    certificate past the device fast path (33 MultiGrants): the host decoder decides it
+    and, with no valid signature, it is rejected."""
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 4, first_cert=77, faults=False)
+    b = s.batch
+    gb = b.grant_bytes[int(b.grant_off[0]):int(b.grant_off[0]) + int(b.grant_len[0])].tobytes()
+    oid = W.grant_object_id(gb)
+    ids = W.SERVER_IDS[:4]
+    ent = [(ids[i % 4] + ("" if i < 4 else f"-{i}"), W.encode_multigrant([(oid, gb)], ids[i % 4], "cl", "",
+                                                                         [(oid, b"\x00" * 256)]))
+           for i in range(33)]
+    m = W.encode_write2(ent, [W.encode_operation(2, oid)])
+    wb = _pack([m])
+    wb.expected_hash = b.expected_hash[:1].copy()
+    for strict in (True, False):
+        g, st = ver.verify_write2(wb, 4, strict)
+        assert st[0] == mh.MSG_FALLBACK
+        assert not g.cert_accept[0] and g.cert_reason[0] == mh.REJECT_NO_GRANT
+    ver.close()
