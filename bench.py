@@ -123,7 +123,10 @@ def main():
     strict = not args.client_predicate
     total_grants = args.grants_total or cfg["grants"]
     C_total = W.n_certs_for_grants(total_grants, R, k)
-    c_lo, c_hi = (C_total * rank) // world, (C_total * (rank + 1)) // world  # this rank's certificate shard
+    # this rank's certificate shard: libmochi_hip's plan (contiguous, 32-aligned, so the
+    # per-rank verdict bitmaps concatenate word by word after the all-gather)
+    plan = mh.shard_plan(C_total, world)
+    c_lo, c_hi = int(plan[rank]), int(plan[rank + 1])
     C = c_hi - c_lo
     # CPU baseline (rank 0, N = 1 only): a child process started BEFORE this
     # process touches the GPU (it forks its workers and must hold no HIP
@@ -136,10 +139,16 @@ def main():
         cpu_child = start_cpu_baseline(args, R, k, cpu_flags, batch_file)
     torch.cuda.set_device(local_rank)
     dist = None
+    comm = None
     if world > 1:
         import torch.distributed as dist
 
+        # torch.distributed only for the rendezvous, barriers and the timing reduction; the
+        # verdict all-gather goes through libmochi_hip's own RCCL communicator (mochi_comm)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        uid = [mh.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = mh.Comm(uid[0], world, rank, local_rank)
 
     # SURVEY §8d stream, unique grant bytes per certificate, signed on this GPU (k_rsa_sign)
     t_gen = time.perf_counter()
@@ -157,14 +166,17 @@ def main():
     ver = mh.Verifier(moduli, device=local_rank)
     ver.moduli = moduli  # for the second context of the pipelined wire leg
     dev = mh.DeviceBatch(batch, local_rank)
-    out = mh.DeviceVerdicts(dev.n_grants, dev.n_certs, local_rank, full=True)
+    out = mh.DeviceVerdicts(dev.n_grants, dev.n_certs, local_rank, full=True, n_ops=dev.n_ops)
     stream = torch.cuda.current_stream()
-    import shard
+    words = mh.shard_words(plan)  # equal all-gather slots; this rank's bitmap fills the head of its slot
+    out.cert_accept_bits = torch.zeros(words, dtype=torch.int32, device="cuda")
+    gathered = torch.zeros(world * words, dtype=torch.int32, device="cuda")
 
     def step():
         ver.verify_device(dev, out, R, strict, stream=stream.cuda_stream)
-        if dist is not None:  # the only collective: RCCL all-gather of the verdict bitmaps
-            return shard.allgather_bitmaps(out.cert_accept_bits, world)
+        if comm is not None:  # the only collective: RCCL all-gather of the verdict bitmaps
+            comm.allgather_bits(out.cert_accept_bits, gathered, stream.cuda_stream)
+            return gathered
         return out.cert_accept_bits
 
     for _ in range(args.warmup):
@@ -249,7 +261,8 @@ def main():
                 "certs_per_gpu": C,
                 "replication_factor": R,
                 "majority": mh.majority(R),
-                "parallelism": f"dp{world}: contiguous certificate-index shards + RCCL all-gather of verdict bitmaps"
+                "parallelism": f"dp{world}: contiguous 32-aligned certificate shards (mochi_shard_plan) + one "
+                               "RCCL all-gather of the verdict bitmaps through libmochi_hip (mochi_comm)"
                                if world > 1 else "dp1",
             },
             "roofline": roofline(N, stage_ms[2], traffic),
@@ -267,7 +280,13 @@ def main():
             "wall_s": round(wall_max, 4),
         }
     if dist is not None:
+        # the gathered bitmap is the whole batch's: rank 0 checks it holds its own shard's verdicts
+        if rank == 0 and result is not None:
+            g = mh.bits_assemble(plan, gathered.cpu().numpy().view(np.uint32))
+            result["gathered_bitmap_matches_rank0"] = bool(np.array_equal(
+                mh.unpack_bits(g, C_total)[:C], host.cert_accept[:C]))
         dist.barrier()
+        comm.close()
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)

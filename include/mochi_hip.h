@@ -508,6 +508,61 @@ int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs);
 /* Drains pending requests, then stops the flusher. */
 void mochi_batcher_destroy(mochi_batcher* b);
 
+/* ------------------------------------------------------------------------
+ * Multi-GPU: certificates are independent, so a batch is cut
+ * into contiguous certificate ranges, one per GPU, every boundary a multiple of
+ * 32 certificates (the per-GPU accept bitmaps then concatenate word by word).
+ * The only collective is one RCCL all-gather of those bitmaps over xGMI, after
+ * which every GPU holds the whole batch's verdict bitmap.
+ * ------------------------------------------------------------------------ */
+
+/* Shard plan: cert_lo[n_shards+1], shard s = [cert_lo[s], cert_lo[s+1]), every
+ * inner boundary a multiple of 32, the shards' work as even as that allows
+ * (work = grants via cert_grant_off[C+1]; NULL = certificates).  Host only. */
+int mochi_shard_plan(uint32_t n_certs, const uint32_t* cert_grant_off, uint32_t n_shards, uint32_t* cert_lo);
+/* Words per shard slot of the all-gather (max over shards of ceil(size/32)). */
+uint32_t mochi_shard_words(uint32_t n_shards, const uint32_t* cert_lo);
+/* The batch's accept bitmap from an all-gathered buffer of n_shards slots of
+ * words_per_shard words (slot s = shard s's bitmap, zero-padded). */
+int mochi_bits_assemble(uint32_t n_shards, const uint32_t* cert_lo, uint32_t words_per_shard, const uint32_t* gathered,
+                        uint32_t* bits_out);
+
+/* One process owning several GPUs (e.g. one JVM server on an 8-GPU node):
+ * bit i of device_mask = HIP device i; one context per device, each driven by
+ * its own host thread, and an RCCL communicator over them (ncclCommInitAll). */
+typedef struct mochi_mctx mochi_mctx;
+mochi_mctx* mochi_mctx_create(uint64_t device_mask, const uint8_t* moduli_be, uint32_t n_keys, uint32_t key_bytes,
+                              uint32_t public_exponent);
+void mochi_mctx_destroy(mochi_mctx* m);
+/* Device ids of the context (returns their count). */
+int mochi_mctx_devices(mochi_mctx* m, int* devices, int max);
+/* The per-device context i (profiling, chunk size, ...); owned by m. */
+mochi_ctx* mochi_mctx_context(mochi_mctx* m, int i);
+int mochi_mctx_set_server_ids(mochi_mctx* m, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids);
+/* Host batch across the devices: each device runs mochi_verify_batch on its
+ * shard (outputs land in their slices of `out`; grant_valid_bits is not
+ * supported here, use grant_flags), then the shard bitmaps are all-gathered and
+ * out->cert_accept_bits is assembled from device 0's copy. */
+int mochi_mverify_batch(mochi_mctx* m, const mochi_batch* batch, const mochi_params* params, mochi_verdicts* out);
+/* Write2ToServer messages across the devices (shards by wire bytes). */
+int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* batch, const mochi_params* params,
+                         mochi_verdicts* out, uint8_t* msg_status);
+/* After a call: device i's all-gathered buffer (n_devices slots of
+ * words_per_device words, device memory of device i). */
+int mochi_mctx_gathered_bits(mochi_mctx* m, int i, const uint32_t** d_bits, uint32_t* words_per_device);
+
+/* One process per GPU (torchrun / MPI style).  Rank 0 makes the 128-byte id,
+ * the caller moves it to every rank by any transport, each rank joins. */
+#define MOCHI_COMM_ID_BYTES 128
+typedef struct mochi_comm mochi_comm;
+int mochi_comm_unique_id(uint8_t* id_out /* [128] */);
+mochi_comm* mochi_comm_init(const uint8_t* id /* [128] */, int n_ranks, int rank, int device);
+/* ncclAllGather of words_per_rank uint32 per rank: d_recv[n_ranks * words_per_rank]
+ * (d_send may be d_recv + rank * words_per_rank), async on `stream`. */
+int mochi_comm_allgather_bits(mochi_comm* c, const uint32_t* d_send, uint32_t words_per_rank, uint32_t* d_recv,
+                              void* stream);
+void mochi_comm_destroy(mochi_comm* c);
+
 #ifdef __cplusplus
 }
 #endif

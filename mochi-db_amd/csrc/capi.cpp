@@ -158,6 +158,13 @@ int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
 
 }  // namespace
 
+namespace mochi {
+int set_error(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+}  // namespace mochi
+
 struct mochi_ctx {
   int device = 0;
   hipStream_t stream = nullptr;

@@ -46,7 +46,8 @@ struct ByteReader {
 // which restates MochiProtocol.java:7369-7425 + protobuf-java 3.16.3
 // CodedInputStream.  Returns 1 ok / 0 malformed.
 // ---------------------------------------------------------------------------
-constexpr int kMaxGroupDepth = 16;
+constexpr int kMaxGroupDepth = 16;    // register-resident group stack of the fast path
+constexpr int kDeepGroupDepth = 100;  // CodedInputStream's default recursion limit (protobuf-java)
 
 __device__ __forceinline__ bool rd_varint(ByteReader& r, uint32_t& pos, uint64_t& v) {
   uint64_t x = 0;
@@ -128,12 +129,16 @@ __device__ __forceinline__ bool rd_string(ByteReader& r, uint32_t& pos, uint32_t
   return true;
 }
 
-__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
-                                   uint32_t& oid_len) {
+// kDepth = size of the unknown-group stack.  The fast instance keeps 16 entries
+// in registers and reports a deeper nesting through `too_deep`; parse_grant
+// then re-parses with the 100-deep instance, kept out of line (scratch stack).
+template <int kDepth>
+__device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
+                                     uint32_t& oid_off, uint32_t& oid_len, bool& too_deep) {
   uint32_t pos = 0;
   int64_t t = 0;
   uint32_t hoff = 0, hlen = 0, ooff = 0, olen = 0;
-  uint32_t stack[kMaxGroupDepth];
+  uint32_t stack[kDepth];
   int depth = 0;
 #pragma unroll 1
   while (pos < r.len) {
@@ -182,7 +187,10 @@ __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_of
         break;
       }
       case 3:
-        if (depth >= kMaxGroupDepth) return false;
+        if (depth >= kDepth) {
+          too_deep = kDepth < kDeepGroupDepth;
+          return false;
+        }
         stack[depth++] = field;
         break;
       case 5:
@@ -200,6 +208,19 @@ __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_of
   oid_off = ooff;
   oid_len = olen;
   return true;
+}
+
+__device__ __noinline__ bool parse_grant_deep(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
+                                              uint32_t& oid_off, uint32_t& oid_len) {
+  bool unused = false;
+  return parse_grant_t<kDeepGroupDepth>(r, ts, hash_off, hash_len, oid_off, oid_len, unused);
+}
+
+__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
+                                   uint32_t& oid_len) {
+  bool too_deep = false;
+  if (parse_grant_t<kMaxGroupDepth>(r, ts, hash_off, hash_len, oid_off, oid_len, too_deep)) return true;
+  return too_deep && parse_grant_deep(r, ts, hash_off, hash_len, oid_off, oid_len);
 }
 
 __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {

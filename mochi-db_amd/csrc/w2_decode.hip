@@ -72,7 +72,7 @@ __device__ __forceinline__ bool vlen(ByteReader& r, uint32_t& pos, uint32_t end,
 // Skip an unknown group opened by `field` (skipMessage + checkLastTagWas).
 // Rare: kept out of line so its stack does not weigh on the common path.
 __device__ __noinline__ bool skip_group(ByteReader& r, uint32_t& pos, uint32_t end, uint32_t field) {
-  uint32_t stack[kMaxGroupDepth];
+  uint32_t stack[kDeepGroupDepth];
   int depth = 1;
   stack[0] = field;
 #pragma unroll 1
@@ -97,7 +97,7 @@ __device__ __noinline__ bool skip_group(ByteReader& r, uint32_t& pos, uint32_t e
         pos += l;
         break;
       case 3:
-        if (depth >= kMaxGroupDepth) return false;
+        if (depth >= kDeepGroupDepth) return false;
         stack[depth++] = f;
         break;
       case 4:

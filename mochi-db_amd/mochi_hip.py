@@ -188,6 +188,26 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_batcher_verify.argtypes = [vp, vp, u32, vp, u32, vp, vp]
     lib.mochi_batcher_stats.argtypes = [vp, vp, vp]
     lib.mochi_batcher_destroy.argtypes = [vp]
+    lib.mochi_shard_plan.argtypes = [u32, vp, u32, vp]
+    lib.mochi_shard_words.restype = u32
+    lib.mochi_shard_words.argtypes = [u32, vp]
+    lib.mochi_bits_assemble.argtypes = [u32, vp, u32, vp, vp]
+    lib.mochi_mctx_create.restype = vp
+    lib.mochi_mctx_create.argtypes = [ctypes.c_uint64, vp, u32, u32, u32]
+    lib.mochi_mctx_destroy.argtypes = [vp]
+    lib.mochi_mctx_devices.argtypes = [vp, vp, ctypes.c_int]
+    lib.mochi_mctx_context.restype = vp
+    lib.mochi_mctx_context.argtypes = [vp, ctypes.c_int]
+    lib.mochi_mctx_set_server_ids.argtypes = [vp, vp, vp, u32]
+    lib.mochi_mverify_batch.argtypes = [vp, vp, vp, vp]
+    lib.mochi_mverify_write2.argtypes = [vp, vp, vp, vp, vp]
+    lib.mochi_mctx_gathered_bits.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                             ctypes.POINTER(ctypes.c_uint32)]
+    lib.mochi_comm_unique_id.argtypes = [vp]
+    lib.mochi_comm_init.restype = vp
+    lib.mochi_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.mochi_comm_allgather_bits.argtypes = [vp, vp, u32, vp, vp]
+    lib.mochi_comm_destroy.argtypes = [vp]
     lib.mochi_host_alloc.restype = vp
     lib.mochi_host_alloc.argtypes = [ctypes.c_uint64]
     lib.mochi_host_free.argtypes = [vp]
@@ -903,3 +923,127 @@ class DeviceSigner:
             self.lib.mochi_signer_destroy(self.h)
             self.h = None
 
+
+
+# ---------------------------------------------------------------------------
+# Multi-GPU (include/mochi_hip.h)
+# ---------------------------------------------------------------------------
+def shard_plan(n_certs: int, n_shards: int, cert_grant_off: Optional[np.ndarray] = None) -> np.ndarray:
+    """Contiguous 32-aligned certificate shards (mochi_shard_plan): cert_lo[n_shards+1]."""
+    lib = load_library()
+    out = np.zeros(n_shards + 1, np.uint32)
+    cgo = None if cert_grant_off is None else np.ascontiguousarray(cert_grant_off, np.uint32)
+    if lib.mochi_shard_plan(n_certs, _ptr(cgo), n_shards, _ptr(out)) != OK:
+        raise MochiError("mochi_shard_plan failed")
+    return out
+
+
+def shard_words(cert_lo: np.ndarray) -> int:
+    lo = np.ascontiguousarray(cert_lo, np.uint32)
+    return int(load_library().mochi_shard_words(lo.shape[0] - 1, _ptr(lo)))
+
+
+def bits_assemble(cert_lo: np.ndarray, gathered: np.ndarray) -> np.ndarray:
+    """The batch's accept bitmap from the all-gathered per-shard slots (mochi_bits_assemble)."""
+    lo = np.ascontiguousarray(cert_lo, np.uint32)
+    g = np.ascontiguousarray(gathered, np.uint32)
+    n = lo.shape[0] - 1
+    out = np.zeros(max(1, (int(lo[-1]) + 31) // 32), np.uint32)
+    if load_library().mochi_bits_assemble(n, _ptr(lo), g.shape[0] // n, _ptr(g), _ptr(out)) != OK:
+        raise MochiError("mochi_bits_assemble failed")
+    return out[:(int(lo[-1]) + 31) // 32]
+
+
+class MultiVerifier:
+    """mochi_mctx: one process, the GPUs of device_mask, one context + host thread
+    each, RCCL all-gather of the verdict bitmaps."""
+
+    def __init__(self, moduli_be, device_mask: int):
+        self.lib = load_library()
+        mod = np.ascontiguousarray(np.frombuffer(b"".join(bytes(m) for m in moduli_be), np.uint8))
+        self._mod = mod
+        self.h = self.lib.mochi_mctx_create(device_mask, mod.ctypes.data, mod.size // RSA_BYTES, RSA_BYTES, RSA_E)
+        if not self.h:
+            raise MochiError(f"mochi_mctx_create: {_err(self.lib)}")
+        devs = (ctypes.c_int * 64)()
+        self.devices = list(devs)[:self.lib.mochi_mctx_devices(self.h, devs, 64)]
+
+    def set_server_ids(self, server_ids) -> None:
+        enc = [x.encode() if isinstance(x, str) else bytes(x) for x in server_ids]
+        blob = np.frombuffer(b"".join(enc) or b"\x00", np.uint8).copy()
+        off = np.zeros(len(enc) + 1, np.uint32)
+        np.cumsum([len(x) for x in enc], out=off[1:])
+        if self.lib.mochi_mctx_set_server_ids(self.h, _ptr(blob), _ptr(off), len(enc)) != OK:
+            raise MochiError(_err(self.lib))
+
+    def verify(self, batch: Batch, replication_factor: int, strict_gt: bool = True, quorum_mode: int = 0) -> Verdicts:
+        b = batch.normalized()
+        out = Verdicts.alloc(b.n_grants, b.n_certs, b.n_ops)
+        bc, vc = b.to_c(), out.to_c()
+        vc.grant_valid_bits = None
+        p = params(replication_factor, strict_gt, quorum_mode)
+        rc = self.lib.mochi_mverify_batch(self.h, ctypes.byref(bc), ctypes.byref(p), ctypes.byref(vc))
+        if rc != OK:
+            raise MochiError(f"mochi_mverify_batch rc={rc}: {_err(self.lib)}")
+        out.grant_valid_bits = np.zeros_like(out.grant_valid_bits)
+        return out
+
+    def verify_write2(self, wb, replication_factor: int, strict_gt: bool = True, quorum_mode: int = 0):
+        wc, keep = write2_batch_c(wb)
+        M = wb.n_msgs
+        O = int(wb.op_flags_off[-1]) if wb.op_flags_off is not None else 0
+        out = Verdicts.alloc(0, M, O)
+        vc = out.to_c()
+        vc.grant_valid_bits = vc.grant_flags = vc.grant_ts = None
+        if wb.op_flags_off is None:
+            vc.op_decision = vc.op_g0 = vc.op_ts = None
+        p = params(replication_factor, strict_gt, quorum_mode)
+        st = np.zeros(max(M, 1), np.uint8)
+        rc = self.lib.mochi_mverify_write2(self.h, ctypes.addressof(wc), ctypes.addressof(p), ctypes.addressof(vc),
+                                           _ptr(st))
+        if rc != OK:
+            raise MochiError(f"mochi_mverify_write2 rc={rc}: {_err(self.lib)}")
+        return out, st[:M].copy()
+
+    def gathered_bits(self, i: int):
+        """(device pointer, words per device slot) of device i's all-gathered buffer."""
+        p, w = ctypes.c_void_p(), ctypes.c_uint32()
+        if self.lib.mochi_mctx_gathered_bits(self.h, i, ctypes.byref(p), ctypes.byref(w)) != OK:
+            raise MochiError(_err(self.lib))
+        return p.value, w.value
+
+    def close(self):
+        if self.h:
+            self.lib.mochi_mctx_destroy(self.h)
+            self.h = None
+
+
+class Comm:
+    """mochi_comm: one process per GPU; the verdict-bitmap all-gather through librccl."""
+
+    def __init__(self, unique_id: bytes, n_ranks: int, rank: int, device: int):
+        self.lib = load_library()
+        idb = ctypes.create_string_buffer(bytes(unique_id), 128)
+        self.h = self.lib.mochi_comm_init(idb, n_ranks, rank, device)
+        if not self.h:
+            raise MochiError(f"mochi_comm_init: {_err(self.lib)}")
+        self.n_ranks = n_ranks
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load_library()
+        b = ctypes.create_string_buffer(128)
+        if lib.mochi_comm_unique_id(b) != OK:
+            raise MochiError(f"mochi_comm_unique_id: {_err(lib)}")
+        return b.raw
+
+    def allgather_bits(self, local_t, out_t, stream: int = 0) -> None:
+        """int32 torch tensors: local [W] -> out [n_ranks * W] (async on `stream`)."""
+        rc = self.lib.mochi_comm_allgather_bits(self.h, local_t.data_ptr(), local_t.numel(), out_t.data_ptr(), stream)
+        if rc != OK:
+            raise MochiError(f"mochi_comm_allgather_bits: {_err(self.lib)}")
+
+    def close(self):
+        if self.h:
+            self.lib.mochi_comm_destroy(self.h)
+            self.h = None

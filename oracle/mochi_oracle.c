@@ -159,7 +159,7 @@ static int rd_string(rd_t* r, uint32_t* off, uint32_t* len) {
   return 1;
 }
 
-#define ORACLE_MAX_GROUP_DEPTH 16
+#define ORACLE_MAX_GROUP_DEPTH 100 /* CodedInputStream default recursion limit */
 
 int oracle_grant_parse(const uint8_t* buf, size_t len, oracle_grant_view* out) {
   rd_t r = {buf, len, 0};

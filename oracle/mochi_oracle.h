@@ -50,8 +50,8 @@ typedef struct oracle_grant_view {
  * protobuf-java 3.16.3 CodedInputStream semantics: last value wins, unknown
  * fields skipped by wire type, strings must be valid UTF-8
  * (readStringRequireUtf8), tag 0 / wire types 6,7 / stray END_GROUP /
- * truncated input are errors.  Groups nest at most 16 deep (protobuf-java
- * allows 100; documented deviation).  Returns 1 ok, 0 malformed. */
+ * truncated input are errors.  Unknown groups nest at most 100 deep
+ * (CodedInputStream's default recursion limit).  Returns 1 ok, 0 malformed. */
 int oracle_grant_parse(const uint8_t* buf, size_t len, oracle_grant_view* out);
 
 /* SHA-256 (OpenSSL). */

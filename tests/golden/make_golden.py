@@ -125,6 +125,11 @@ def grant_vectors():
         ("empty", b""),
         ("varint_11_bytes", bytes.fromhex("10" + "ff" * 10 + "01")),
         ("neg_len", bytes.fromhex("0a" + "ffffffff0f")),
+        # unknown groups nested 17 / 99 / 100 / 101 deep (CodedInputStream's recursion limit is 100)
+        ("groups_nested_17", bytes.fromhex("0a016b1005" + "5b" * 17 + "5c" * 17)),
+        ("groups_nested_99", bytes.fromhex("0a016b1005" + "5b" * 99 + "5c" * 99)),
+        ("groups_nested_100", bytes.fromhex("0a016b1005" + "5b" * 100 + "5c" * 100)),
+        ("groups_nested_101", bytes.fromhex("0a016b1005" + "5b" * 101 + "5c" * 101)),
     ]
     parse = []
     for name, data in parse_cases:
@@ -339,6 +344,11 @@ def cert_cases():
 
 
 def main():
+    if sys.argv[1:] == ["grant_vectors"]:  # regenerate only the google.protobuf Grant vectors
+        gv, pv = grant_vectors()
+        with open(os.path.join(HERE, "grant_vectors.json"), "w") as f:
+            json.dump({"encode": gv, "parse": pv}, f, indent=1)
+        return
     if sys.argv[1:] == ["cert_cases"]:  # regenerate only the hand-constructed verdict cases
         with open(os.path.join(HERE, "cert_cases.json"), "w") as f:
             json.dump(cert_cases(), f, indent=1)

@@ -398,3 +398,28 @@ def test_host_pipeline_chunking(pool4, chunk):
     gs = ver.verify(_scatter_blob(s.batch, chunk), 4, True)
     assert_same(gs, o, f"scattered chunk={chunk}")
     ver.close()
+
+
+def test_grant_group_depth_matches_google_protobuf(pool4, ver4, golden_dir):
+    """Unknown groups nested up to CodedInputStream's recursion limit (100) parse on the
+    device (the 16-deep register stack hands deeper grants to the out-of-line 100-deep
+    parser), 101 is malformed -- exactly google.protobuf's verdicts."""
+    d = json.load(open(os.path.join(golden_dir, "grant_vectors.json")))
+    vecs = [v for v in d["parse"] if v["name"].startswith("groups_nested") or v["name"] == "group_skipped"]
+    assert len(vecs) == 5
+    pem = W.load_keys(1)[0]
+    msgs = [bytes.fromhex(v["bytes"]) for v in vecs]
+    n = len(msgs)
+    blob = np.frombuffer(b"".join(msgs), np.uint8).copy()
+    off = np.cumsum([0] + [len(m) for m in msgs[:-1]]).astype(np.uint64)
+    b = mh.Batch(grant_bytes=blob, grant_off=off, grant_len=np.array([len(m) for m in msgs], np.uint32),
+                 sig=np.frombuffer(b"".join(O.rsa_sign(pem, m) for m in msgs), np.uint8).reshape(n, 256).copy(),
+                 signer=np.zeros(n, np.uint16), grant_key=np.zeros(n, np.uint8),
+                 cert_grant_off=np.arange(n + 1, dtype=np.uint32), cert_op_off=np.zeros(n + 1, np.uint32),
+                 op_key=np.zeros(0, np.uint8), op_flags=np.zeros(0, np.uint8), expected_hash=np.zeros((n, 128), np.uint8))
+    g = ver4.verify(b, 4, True)
+    for i, v in enumerate(vecs):
+        assert bool(g.grant_flags[i] & mh.GRANT_PARSED) == v["expect"]["ok"], v["name"]
+        assert g.grant_flags[i] & mh.GRANT_SIG_OK  # signature fine either way
+        if v["expect"]["ok"]:
+            assert g.grant_ts[i] == v["expect"]["timestamp"], v["name"]

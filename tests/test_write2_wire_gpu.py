@@ -261,7 +261,8 @@ def test_batcher_concurrent_callers(pool4, with_flags):
     if with_flags:
         wb.op_flags = wb.op_flags.copy()
         wb.op_flags[::7] = mh.OP_HAS_SVOC  # some ops not local -> WRONG_SHARD, never checked
-    ref, ref_st = ver.verify_write2(wb, 4, True)
+    ids, off = W.server_id_table(4)
+    ref, ref_st = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)  # the oracle, not the library itself
     b = mh.Batcher(ver, 4, True, max_msgs=128, max_wait_us=2000, with_op_flags=with_flags)
     M = wb.n_msgs
     res = [None] * M
