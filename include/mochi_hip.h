@@ -319,6 +319,14 @@ int mochi_tally_responses(uint32_t n_requests, const uint32_t* resp_off, const u
                           const uint64_t* chosen_off, uint32_t replication_factor, int32_t* chosen,
                           uint8_t* reason, uint32_t* accept_bits);
 
+/* The same aggregation on the device, batched across in-flight transactions
+ * (every pointer a device pointer; asynchronous on `stream`, a hipStream_t).
+ * Lane = request.  accept_bits must hold ceil(n_requests/32) words. */
+int mochi_tally_responses_device(uint32_t n_requests, const uint32_t* resp_off, const uint32_t* n_ops,
+                                 const uint32_t* resp_n_ops, const uint64_t* status_off, const uint8_t* status,
+                                 const uint64_t* chosen_off, uint32_t replication_factor, int32_t* chosen,
+                                 uint8_t* reason, uint32_t* accept_bits, void* stream);
+
 /* Write1 response kinds: the ProtocolMessage payload case a Write1ToServer got
  * back (MochiDBClient.java:274-289). */
 #define MOCHI_W1_OK 0             /* WRITE1OKFROMSERVER                        */
@@ -352,6 +360,11 @@ enum mochi_write1_decision {
 int mochi_write1_classify(uint32_t n_requests, const uint32_t* resp_off, const uint8_t* resp_kind,
                           const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
                           const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision);
+/* The Write1 classification on the device (device pointers, async on `stream`). */
+int mochi_write1_classify_device(uint32_t n_requests, const uint32_t* resp_off, const uint8_t* resp_kind,
+                                 const uint32_t* resp_server, const uint32_t* resp_grant_off, const uint8_t* grant_key,
+                                 const int64_t* grant_ts, const uint8_t* grant_status, uint8_t* decision,
+                                 void* stream);
 
 /* ------------------------------------------------------------------------
  * Write2ToServer wire path: the device decodes the received protobuf bytes.

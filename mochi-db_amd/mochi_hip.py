@@ -169,6 +169,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_ctx_read_profile.argtypes = [vp, vp, u32, vp]
     lib.mochi_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
     lib.mochi_write1_classify.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mochi_tally_responses_device.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp, vp]
+    lib.mochi_write1_classify_device.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mochi_ctx_last_total_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     lib.mochi_ctx_set_chunk_grants.argtypes = [vp, u32]
     lib.mochi_ctx_set_server_ids.argtypes = [vp, vp, vp, u32]
@@ -755,6 +757,72 @@ def tally_responses(responses: Sequence[Sequence[Sequence[int]]], n_ops: Sequenc
     acc = unpack_bits(bits, nreq)
     ch = [chosen[int(chosen_off[r]):int(chosen_off[r]) + n_ops[r]].copy() for r in range(nreq)]
     return acc, reason[:nreq].copy(), ch
+
+
+def _pack_responses(responses, n_ops):
+    nreq = len(responses)
+    resp_off = np.zeros(nreq + 1, np.uint32)
+    resp_n_ops, status_off, status, chosen_off = [], [], [], np.zeros(max(nreq, 1), np.uint64)
+    pos = cpos = 0
+    for r, resps in enumerate(responses):
+        resp_off[r + 1] = resp_off[r] + len(resps)
+        chosen_off[r] = cpos
+        cpos += n_ops[r]
+        for st in resps:
+            resp_n_ops.append(len(st))
+            status_off.append(pos)
+            status.extend(st)
+            pos += len(st)
+    return (resp_off, np.asarray(n_ops if len(n_ops) else [0], np.uint32),
+            np.asarray(resp_n_ops if resp_n_ops else [0], np.uint32),
+            np.asarray(status_off if status_off else [0], np.uint64), np.asarray(status if status else [0], np.uint8),
+            chosen_off, max(cpos, 1))
+
+
+def tally_responses_device(responses, n_ops, replication_factor: int, device: int = 0):
+    """Client aggregation on the device (mochi_tally_responses_device), batched over
+    requests; same results as tally_responses.  torch moves the arrays (plumbing)."""
+    import torch
+
+    lib = load_library()
+    nreq = len(responses)
+    resp_off, n_ops_a, rn, so, st, co, nch = _pack_responses(responses, n_ops)
+    d = torch.device("cuda", device)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view({1: np.uint8, 2: np.int16, 4: np.int32,
+                                                                 8: np.int64}[a.dtype.itemsize])).to(d)
+    ts = [t(x) for x in (resp_off, n_ops_a, rn, so, st, co)]
+    chosen = torch.full((nch,), -1, dtype=torch.int32, device=d)
+    reason = torch.zeros(max(nreq, 1), dtype=torch.uint8, device=d)
+    bits = torch.zeros(max((nreq + 31) // 32, 1), dtype=torch.int32, device=d)
+    rc = lib.mochi_tally_responses_device(nreq, *[x.data_ptr() for x in ts[:6]], replication_factor,
+                                          chosen.data_ptr(), reason.data_ptr(), bits.data_ptr(),
+                                          torch.cuda.current_stream(d).cuda_stream)
+    if rc != OK:
+        raise MochiError(f"mochi_tally_responses_device rc={rc}")
+    torch.cuda.synchronize(d)
+    acc = unpack_bits(bits.cpu().numpy().view(np.uint32), nreq)
+    ch_h = chosen.cpu().numpy()
+    ch = [ch_h[int(co[r]):int(co[r]) + n_ops[r]].copy() for r in range(nreq)]
+    return acc, reason.cpu().numpy()[:nreq].copy(), ch
+
+
+def write1_classify_device(requests, device: int = 0) -> np.ndarray:
+    """Client Write1 round outcome per request on the device (mochi_write1_classify_device)."""
+    import torch
+
+    lib = load_library()
+    a = pack_write1(requests)
+    d = torch.device("cuda", device)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view({1: np.uint8, 4: np.int32,
+                                                                 8: np.int64}[x.dtype.itemsize])).to(d)
+    ts = [t(x) for x in a]
+    out = torch.zeros(max(len(requests), 1), dtype=torch.uint8, device=d)
+    rc = lib.mochi_write1_classify_device(len(requests), *[x.data_ptr() for x in ts], out.data_ptr(),
+                                          torch.cuda.current_stream(d).cuda_stream)
+    if rc != OK:
+        raise MochiError(f"mochi_write1_classify_device rc={rc}")
+    torch.cuda.synchronize(d)
+    return out.cpu().numpy()[:len(requests)].copy()
 
 
 # Write1 response kinds / round decisions (include/mochi_hip.h)
