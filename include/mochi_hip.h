@@ -250,11 +250,20 @@ int mochi_verify_batch_device(mochi_ctx* ctx, const mochi_batch* batch, const mo
  * 256 bytes each) under key `signer[i]`, on the device, through the same
  * kernels as the verify path (k_rsa_pow + k_rsa_final).  out_be: n * 256
  * bytes.  out_z (optional, n * 74 words): the squaring-chain intermediate
- * z = s^(2^16) * R^-(2^16-1) mod n in radix-2^28 limbs (< 2n), for tests.
- * Host memory, synchronous.
+ * z = s^(2^16) mod n in radix-2^28 limbs, not fully reduced (< 2^2064), for
+ * tests.  Host memory, synchronous.
  */
 int mochi_rsa_public_op(mochi_ctx* ctx, uint32_t n, const uint8_t* sig_be, const uint16_t* signer, uint8_t* out_be,
                         uint32_t* out_z);
+
+/*
+ * The k_rsa_pow fold matrix of one RSA-2048 modulus (inspection / tests; the
+ * context builds one per key).  img: 102,400 int8 = the MFMA A fragments of
+ * R_{j,b} = 2^(28(73+j)+8b) mod n in balanced mixed-radix digits (layout:
+ * mochi-db_amd/csrc/fold.h); cadd: the int8 bias correction 128 * sum R_{j,b}
+ * as 74 limbs of 28 bits.  Host memory.
+ */
+int mochi_fold_matrix(const uint8_t* modulus_be, int8_t* img, uint32_t* cadd);
 
 /*
  * Per-stage device timing.  While profiling is on, every verify call records a

@@ -116,9 +116,9 @@ int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
   uint32_t inv = 1;
   for (int i = 0; i < 6; i++) inv *= 2u - e->n32[0] * inv;
   e->n0inv = (0u - inv) & kLimbMask;
-  // Per-key constants (R = 2^(28*74)):
-  //   kfix = R^65537 mod n                       (k_rsa_raw: z*K*s = s^65537)
-  //   q    = R^-(2^16) mod n                     (k_rsa_final: MontMul(z, s) = s^65537 * q)
+  // Per-key constants (R = 2^(28*74)); k_rsa_pow leaves z = s^(2^16) mod n:
+  //   kfix = R^2 mod n                           (k_rsa_raw: MontMul(MontMul(z, K), s) = s^65537)
+  //   q    = R^-1 mod n                          (k_rsa_final: MontMul(z, s) = s^65537 * q)
   //   a2   = (Cpad * q mod n) + 2n               (k_rsa_final: target EM*q = Cpad*q + H*q)
   // Cpad = EMSA-PKCS1-v1_5 encoding (RFC 8017 §9.2) of SHA-256 with an all-zero digest.
   uint8_t cpad[256];
@@ -135,8 +135,8 @@ int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
          *q = BN_new(), *a2 = BN_new(), *cp = BN_bin2bn(cpad, 256, nullptr), *n2 = BN_new();
   int ok = ctx && n && r && k && ex && t && q && a2 && cp && n2;
   ok = ok && BN_set_bit(r, kL * kLimbBits) && BN_mod(r, r, n, ctx);
-  ok = ok && BN_set_word(ex, MOCHI_RSA_E) && BN_mod_exp(k, r, ex, n, ctx);
-  ok = ok && BN_set_word(ex, 1u << 16) && BN_mod_exp(t, r, ex, n, ctx) && BN_mod_inverse(q, t, n, ctx) != nullptr;
+  ok = ok && BN_mod_mul(k, r, r, n, ctx);
+  ok = ok && BN_copy(t, r) && BN_mod_inverse(q, t, n, ctx) != nullptr;
   ok = ok && BN_mod_mul(a2, cp, q, n, ctx) && BN_lshift1(n2, n) && BN_add(a2, a2, n2);
   auto to_limbs_bn = [](const BIGNUM* v, uint32_t* x) {
     uint8_t le[264];
@@ -156,6 +156,59 @@ int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
   return MOCHI_OK;
 }
 
+// Fold matrix of k_rsa_pow (fold.h): R_{j,b} = 2^(28(73+j)+8b) mod n as balanced
+// mixed-radix digits (8, 8, 8, 4 bits per 28-bit limb), laid out as MFMA A fragments.
+int make_fold_key(const uint8_t* n_be, mochi::FoldKey* f) {
+  using namespace mochi;
+  memset(f, 0, sizeof *f);
+  static thread_local std::vector<int8_t> W;  // [296 rows][300 k]
+  constexpr int kRows = kFoldLimbs * 4, kK = kFoldNH * 4;
+  W.assign((size_t)kRows * kK, 0);
+  BN_CTX* ctx = BN_CTX_new();
+  BIGNUM *n = BN_bin2bn(n_be, 256, nullptr), *r = BN_new(), *sum = BN_new();
+  int ok = ctx && n && r && sum;
+  if (ok) BN_zero(sum);
+  ok = ok && BN_set_bit(r, kLimbBits * kFoldF) && BN_mod(r, r, n, ctx);
+  uint8_t le[264];
+  for (int k = 0; k < kK && ok; k++) {
+    if (k) ok = BN_lshift(r, r, (k & 3) ? 8 : 4) && BN_mod(r, r, n, ctx);  // limb = 8 + 8 + 8 + 4 bits
+    ok = ok && BN_add(sum, sum, r) && BN_bn2lebinpad(r, le, sizeof le) == (int)sizeof le;
+    int carry = 0;
+    for (int row = 0; row < kRows && ok; row++) {
+      const int bit = 28 * (row >> 2) + 8 * (row & 3), w = (row & 3) == 3 ? 4 : 8;
+      const int field = (int)((((uint32_t)le[bit >> 3] | (uint32_t)le[(bit >> 3) + 1] << 8) >> (bit & 7)) & ((1u << w) - 1));
+      int d = field + carry;
+      carry = d >= (1 << (w - 1));
+      if (carry) d -= 1 << w;
+      W[(size_t)row * kK + k] = (int8_t)d;
+    }
+    ok = ok && carry == 0;
+  }
+  // cadd = 128 * sum R_{j,b} as 74 limbs of 28 bits
+  ok = ok && BN_lshift(sum, sum, 7) && BN_num_bits(sum) <= kLimbBits * kFoldLimbs &&
+       BN_bn2lebinpad(sum, le, sizeof le) == (int)sizeof le;
+  for (int q = 0; q < kFoldLimbs && ok; q++) {
+    const int bit = q * kLimbBits, by = bit >> 3;
+    uint64_t w = 0;
+    for (int b = 0; b < 5 && by + b < (int)sizeof le; b++) w |= (uint64_t)le[by + b] << (8 * b);
+    f->cadd[q] = (uint32_t)(w >> (bit & 7)) & kLimbMask;
+  }
+  BN_free(n);
+  BN_free(r);
+  BN_free(sum);
+  BN_CTX_free(ctx);
+  if (!ok) return fail(MOCHI_EINVAL, "fold matrix precompute failed");
+  for (int mt = 0; mt < kFoldMT; mt++)
+    for (int ks = 0; ks < kFoldKS; ks++)
+      for (int lane = 0; lane < 64; lane++)
+        for (int jj = 0; jj < 16; jj++) {
+          const int row = 32 * mt + (lane & 31), limb = 8 * ks + 4 * (lane >> 5) + jj / 4;
+          if (row < kRows && limb < kFoldNH)
+            f->img[((mt * kFoldKS + ks) * 64 + lane) * 16 + jj] = W[(size_t)row * kK + 4 * limb + jj % 4];
+        }
+  return MOCHI_OK;
+}
+
 }  // namespace
 
 namespace mochi {
@@ -170,6 +223,7 @@ struct mochi_ctx {
   hipStream_t stream = nullptr;
   uint32_t n_keys = 0;
   mochi::KeyEntry* d_keys = nullptr;
+  mochi::FoldKey* d_fold = nullptr;  // per-key k_rsa_pow fold matrices (~101 KB each)
   std::mutex mu;
   // verify scratch
   DevBuf digest, ts, hash_off, hash_len, flags, count, cursor, total, perm, xbuf;
@@ -256,8 +310,11 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
     return nullptr;
   }
   std::vector<mochi::KeyEntry> table(n_keys);
+  std::vector<mochi::FoldKey> fold(n_keys);
   for (uint32_t k = 0; k < n_keys; k++)
-    if (make_key_entry(moduli_be + (size_t)k * MOCHI_RSA_BYTES, &table[k]) != MOCHI_OK) return nullptr;
+    if (make_key_entry(moduli_be + (size_t)k * MOCHI_RSA_BYTES, &table[k]) != MOCHI_OK ||
+        make_fold_key(moduli_be + (size_t)k * MOCHI_RSA_BYTES, &fold[k]) != MOCHI_OK)
+      return nullptr;
   mochi_ctx* c = new mochi_ctx;
   c->device = device;
   c->n_keys = n_keys;
@@ -273,7 +330,9 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
             hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming) == hipSuccess &&
             hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_keys, sizeof(mochi::KeyEntry) * n_keys) == hipSuccess &&
-            hipMemcpy(c->d_keys, table.data(), sizeof(mochi::KeyEntry) * n_keys, hipMemcpyHostToDevice) == hipSuccess;
+            hipMemcpy(c->d_keys, table.data(), sizeof(mochi::KeyEntry) * n_keys, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMalloc(&c->d_fold, sizeof(mochi::FoldKey) * n_keys) == hipSuccess &&
+            hipMemcpy(c->d_fold, fold.data(), sizeof(mochi::FoldKey) * n_keys, hipMemcpyHostToDevice) == hipSuccess;
   for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   (void)hipSetDevice(save);
   if (!ok) {
@@ -304,6 +363,7 @@ void mochi_ctx_destroy(mochi_ctx* c) {
   if (c->ev_tot) (void)hipEventDestroy(c->ev_tot);
   if (c->s_out) (void)hipStreamDestroy(c->s_out);
   if (c->d_keys) (void)hipFree(c->d_keys);
+  if (c->d_fold) (void)hipFree(c->d_fold);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   (void)hipSetDevice(save);
@@ -417,6 +477,7 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.majority = 2 * (R / 3) + 1;  // ClusterConfiguration.getServerMajority  ClusterConfiguration.java:264-267
   a.strict_gt = p->strict_gt ? 1 : 0;
   a.keys = c->d_keys;
+  a.fold = c->d_fold;
   a.digest = c->digest.as<uint32_t>();
   a.ts = o->grant_ts ? o->grant_ts : c->ts.as<int64_t>();
   a.hash_off = c->hash_off.as<uint64_t>();
@@ -1404,6 +1465,17 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   return MOCHI_OK;
 }
 
+int mochi_fold_matrix(const uint8_t* modulus_be, int8_t* img, uint32_t* cadd) {
+  if (!modulus_be || !img || !cadd) return fail(MOCHI_EINVAL, "null argument");
+  if (!(modulus_be[0] & 0x80) || !(modulus_be[255] & 1)) return fail(MOCHI_EINVAL, "modulus must be odd, 2048 bits");
+  std::vector<mochi::FoldKey> f(1);
+  int rc = make_fold_key(modulus_be, f.data());
+  if (rc) return rc;
+  memcpy(img, f[0].img, sizeof f[0].img);
+  memcpy(cadd, f[0].cadd, sizeof f[0].cadd);
+  return MOCHI_OK;
+}
+
 int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const uint16_t* signer, uint8_t* out_be,
                         uint32_t* out_z) {
   if (!c || (n && (!sig_be || !signer || !out_be))) return fail(MOCHI_EINVAL, "null argument");
@@ -1436,6 +1508,7 @@ int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const u
   a.sig = din;
   a.signer = dsigner;
   a.keys = c->d_keys;
+  a.fold = c->d_fold;
   a.digest = c->digest.as<uint32_t>();
   a.flags = c->flags.as<uint8_t>();
   a.count = c->count.as<uint32_t>();

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fold.h"
+
 namespace mochi {
 
 struct KeyEntry;
@@ -29,6 +31,7 @@ struct LaunchArgs {
   const uint32_t* op_key_len;    // [O] or null
   uint32_t majority, strict_gt, quorum_mode;
   const KeyEntry* keys;
+  const FoldKey* fold;  // per-key fold matrices (k_rsa_pow)
   // scratch (context-owned)
   uint32_t* digest;    // [8][N]
   int64_t* ts;         // [N]
@@ -64,9 +67,10 @@ struct LaunchArgs {
 // Stages timed when LaunchArgs::prof_events is set.
 enum ProfStage { kStagePrep = 0, kStageBucket, kStagePow, kStageFinal, kStageTally, kProfStages };
 
-// Slots of the signer-bucketed RSA grid: every bucket is padded to 64.
+// Slots of the signer-bucketed RSA grid: every bucket is padded to kBucketAlign
+// (one k_rsa_pow block of one signer).
 inline uint64_t slot_capacity(uint32_t n_grants, uint32_t n_keys) {
-  return (uint64_t)n_grants + 64ull * (n_keys < n_grants ? n_keys : n_grants);
+  return (uint64_t)n_grants + (uint64_t)kBucketAlign * (n_keys < n_grants ? n_keys : n_grants);
 }
 
 // Write2ToServer wire decode (w2_decode.hip).  Device pointers.

@@ -3,11 +3,11 @@
 //   k_grant_prep    per grant (certificate order): proto3 Grant parse
 //                   (MochiProtocol.java:7369-7425 semantics) + SHA-256 of the
 //                   grant bytes (the signed message)
-//   k_bucket_*      counting sort of grants by signer into 64-aligned buckets,
-//                   so every wavefront of the RSA kernels has ONE modulus
-//                   (wave-uniform -> scalar loads / SGPR operands)
-//   k_rsa_pow       X = (s * R)^(2^16) in Montgomery form (1 mul + 16 sqr)
-//   k_rsa_final     Y = X * s * R^-1 = s^65537 mod n; compare with the
+//   k_bucket_*      counting sort of grants by signer into 512-aligned buckets,
+//                   so every k_rsa_pow block (8 waves) has ONE modulus and fold
+//                   matrix, and every wave of k_rsa_final one modulus (SGPRs)
+//   k_rsa_pow       z = s^(2^16) mod n, 16 squarings, reduction on MFMA (rsa_pow.hip)
+//   k_rsa_final     u = MontMul(z, s) = s^65537 R^-1; compare with the
 //                   EMSA-PKCS1-v1_5 encoding of SHA-256(grant); s < n check
 //   k_tally         per certificate: processMultiGrantsFromAllServers +
 //                   write2apply verdict (InMemoryDataStore.java:576-640)
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void k_grant_prep(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// Signer buckets (64-aligned) — counting sort.
+// Signer buckets (kBucketAlign = 512-aligned: one k_rsa_pow block) — counting sort.
 // ---------------------------------------------------------------------------
 // Wave-aggregated LDS counter add: the lanes of a wave that share a key are
 // ranked by ballot and their leader adds the group's size once, so a batch
@@ -96,14 +96,14 @@ __global__ __launch_bounds__(256) void k_bucket_count(const uint16_t* __restrict
     if (hist[k]) atomicAdd(&count[k], hist[k]);
 }
 
-// Single block: exclusive scan of round_up(count, 64); cursor[k] = start[k].
+// Single block: exclusive scan of round_up(count, kBucketAlign); cursor[k] = start[k].
 __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t* __restrict__ count, uint32_t n_keys,
                                                      uint32_t* __restrict__ cursor, uint32_t* __restrict__ total) {
   __shared__ uint32_t part[256];
   const uint32_t per = (n_keys + 255) / 256;
   const uint32_t b = threadIdx.x * per;
   uint32_t s = 0;
-  for (uint32_t k = b; k < b + per && k < n_keys; k++) s += (count[k] + 63u) & ~63u;
+  for (uint32_t k = b; k < b + per && k < n_keys; k++) s += (count[k] + kBucketAlign - 1) & ~(kBucketAlign - 1);
   part[threadIdx.x] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t* __restrict_
   uint32_t run = part[threadIdx.x];
   for (uint32_t k = b; k < b + per && k < n_keys; k++) {
     cursor[k] = run;
-    run += (count[k] + 63u) & ~63u;
+    run += (count[k] + kBucketAlign - 1) & ~(kBucketAlign - 1);
   }
 }
 

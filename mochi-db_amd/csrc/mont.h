@@ -28,8 +28,8 @@ constexpr int kL = 74;  // 74 * 28 = 2072 bits
 // Per-key device table entry (uploaded once per context).
 struct KeyEntry {
   uint32_t n[kL];     // modulus, 28-bit limbs, little-endian limb order
-  uint32_t kfix[kL];  // R^65537 mod n (R = 2^2072): undoes the R^-(2^16-1) of the squaring chain (k_rsa_raw)
-  uint32_t q[kL];     // Q = R^-(2^16) mod n: the verify target is EM * Q (k_rsa_final)
+  uint32_t kfix[kL];  // R^2 mod n (R = 2^2072): MontMul(z, kfix) = s^(2^16) R, Montgomery form (k_rsa_raw)
+  uint32_t q[kL];     // Q = R^-1 mod n: MontMul(z, s) = s^65537 Q, the verify target is EM * Q (k_rsa_final)
   uint32_t a2[kL];    // (Cpad * Q mod n) + 2n, Cpad = EM with a zero digest (k_rsa_final)
   uint32_t n0inv;     // -n^{-1} mod 2^28
   uint32_t n32[64];   // modulus as 32-bit words, little-endian word order

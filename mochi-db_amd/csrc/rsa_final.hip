@@ -2,8 +2,9 @@
 // EMSA-PKCS1-v1_5 check (RFC 8017 §8.2.2 / §9.2, "SHA256withRSA") with ONE
 // general Montgomery multiply per grant.
 //
-// k_rsa_pow leaves z = s^(2^16) * R^-(2^16-1) (mod n), z < 2n.  Then
-//   u = MontMul(z, s) = s^65537 * Q (mod n),   Q = R^-(2^16) mod n,  u < 2n.
+// k_rsa_pow leaves z = s^(2^16) (mod n), z < 2^2064 = R / 2^8.  Then
+//   u = MontMul(z, s) = s^65537 * Q (mod n),   Q = R^-1 mod n,
+// u = (z s + m n) / R < (2^-8 + 1) n < 2n.
 // The grant is valid iff s < n and s^65537 mod n == EM.  Both sides lie in
 // [0, n) (EM < 2^2041 < n), so equality <=> u == EM * Q (mod n).  With
 // EM = Cpad + H (Cpad: the fixed padding + DigestInfo, H: the 256-bit digest)

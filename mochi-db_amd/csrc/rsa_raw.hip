@@ -3,7 +3,7 @@
 // bignum arithmetic with it); the verify path uses k_rsa_final (rsa_final.hip),
 // which never materialises s^65537 mod n.
 //
-//   w = MontMul(z, K)  = s^(2^16) * R        (K = R^65537 mod n, wave-uniform)
+//   w = MontMul(z, K)  = s^(2^16) * R        (z = s^(2^16) from k_rsa_pow, K = R^2 mod n)
 //   y = MontMul(w, s)  = s^65537 mod n       (< 2n, reduced once below)
 //   valid = s < n  &&  y == 00 01 FF..FF 00 || DigestInfo(SHA-256) || H
 //

@@ -165,6 +165,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_sign_grants.argtypes = [ctypes.c_char_p, u32, vp, vp, vp, vp, ctypes.c_int]
     lib.mochi_pem_modulus.argtypes = [ctypes.c_char_p, vp]
     lib.mochi_rsa_public_op.argtypes = [vp, u32, vp, vp, vp, vp]
+    lib.mochi_fold_matrix.argtypes = [vp, vp, vp]
     lib.mochi_ctx_set_profiling.argtypes = [vp, ctypes.c_int]
     lib.mochi_ctx_read_profile.argtypes = [vp, vp, u32, vp]
     lib.mochi_tally_responses.argtypes = [u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
@@ -566,6 +567,19 @@ class Verifier:
                                                 stream or None)
         if rc != OK:
             raise MochiError(f"mochi_verify_batch_device rc={rc}: {_err(self.lib)}")
+
+
+def fold_matrix(modulus_be: bytes):
+    """The k_rsa_pow fold matrix of one modulus (mochi_fold_matrix): int8 image
+    [10 M-tiles][10 K-steps][64 lanes][16] and the bias correction cadd uint32[74]."""
+    lib = load_library()
+    m = np.frombuffer(bytes(modulus_be), np.uint8)
+    img = np.zeros((10, 10, 64, 16), np.int8)
+    cadd = np.zeros(74, np.uint32)
+    rc = lib.mochi_fold_matrix(_ptr(m), _ptr(img), _ptr(cadd))
+    if rc != OK:
+        raise MochiError(f"mochi_fold_matrix rc={rc}: {_err(lib)}")
+    return img, cadd
 
 
 def rsa_public_op(verifier: "Verifier", sigs: np.ndarray, signer: np.ndarray, want_z: bool = False):

@@ -85,14 +85,15 @@ def test_rsa_public_op_matches_python_pow():
         sigs.append(s.to_bytes(256, "big"))
         signer.append(k)
     y, z = mh.rsa_public_op(ver, np.frombuffer(b"".join(sigs), np.uint8), np.array(signer), want_z=True)
-    R = 1 << (28 * 74)
     for i in range(len(sigs)):
         N = int.from_bytes(mods[signer[i]], "big")
         s = int.from_bytes(sigs[i], "big")
         assert int.from_bytes(y[i].tobytes(), "big") == pow(s, 65537, N), i
+        # k_rsa_pow's fold chain (csrc/fold.h): z = s^(2^16) mod n, not fully reduced
         zi = sum(int(v) << (28 * j) for j, v in enumerate(z[i]))
-        assert zi < 2 * N
-        assert zi % N == pow(s, 65536, N) * pow(pow(R, 65535, N), -1, N) % N, i
+        assert max(int(v) for v in z[i]) < 1 << 28
+        assert zi < 1 << 2064
+        assert zi % N == pow(s, 65536, N), i
     ver.close()
 
 
