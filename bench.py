@@ -33,15 +33,26 @@ METRIC = "verified grant signatures/sec (1/2/4/8 GPU) + % of INT32 VALU roofline
 
 # Algorithmic work: RSA-2048, e = 65537 -> 17 Montgomery
 # multiplications of 2048-bit operands, each a CIOS modmul over s = 64 32-bit
-# limbs = 2s^2 + s = 8,256 32x32->64 multiply-accumulates.  k_rsa_pow does the
-# 16 squarings (16 x 8,256 MAC per grant); the whole path does 17 x 8,256.
+# limbs = 2s^2 + s = 8,256 32x32->64 multiply-accumulates; the squaring chain
+# (k_rsa_pow) is 16 of them, the whole path 17.
 MAC_PER_MODMUL = 8256
 MAC_PER_GRANT = 17 * MAC_PER_MODMUL  # 140,352
-MAC_POW_PER_GRANT = 16 * MAC_PER_MODMUL  # 132,096
-# Peak: v_mad_u64_u32 issues at half the VALU rate on gfx950 (4 cycles per
-# wave64 instruction): 256 CU x 4 SIMD x 32 lanes / 2 x 2.4 GHz = 3.93e13 MAC/s.
-# microbench/int_peak.hip measured 3.41-3.57e13/s (87-91 %) on MI355X.
+MAC_POW_PER_GRANT = 16 * MAC_PER_MODMUL  # 132,096 (CIOS-equivalent work of the squaring chain)
+# Peak VALU issue: one wave64 v_mad_u64_u32 per 4 cycles per SIMD =
+# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 3.93e13 lane-ops/s (microbench/int_peak.hip
+# measured 3.41-3.57e13 v_mad_u64_u32/s, 87-91 %).
 PEAK_MAC_PER_S = 256 * 4 * 32 / 2 * 2.4e9
+# k_rsa_pow (rsa_pow.hip, csrc/fold.h) per grant and squaring: x^2 on the VALU
+# (2,775 28-bit v_mad_u64_u32, the per-signature product with no shared operand)
+# and the fold t_hi x W on the matrix cores (296 x 300 int8 MACs, 200
+# v_mfma_i32_32x32x32_i8 per 64 grants, each holding the SIMD's issue for 8 cycles
+# = 2 wave-instruction slots = 128 lane-slots).  Its roofline is the SIMD issue
+# port both share: 2,775 + 200 * 128 / 64 = 3,175 lane-slots per grant-squaring.
+POW_SQR = 16
+POW_VALU_MAC = 2775
+POW_MFMA_I8_MAC = 296 * 300
+POW_ISSUE_SLOTS = POW_VALU_MAC + 200 * 128 // 64  # 3,175
+INT8_DENSE_PEAK = 2 * 2.5e15 / 2  # MACs/s: i8 = 2x bf16 dense (MICROARCH.md), 2.5 PFLOP bf16 = 1.25e15 MAC/s
 
 # BASELINE.json configs (index 1..3): total grants, replication factor
 CONFIGS = {
@@ -98,11 +109,25 @@ def timed_steps(step, steps, warmup, stream, dist=None):
 
 
 def roofline(n_grants, pow_ms, traffic=None):
-    achieved = n_grants * MAC_POW_PER_GRANT / (pow_ms / 1e3) if pow_ms > 0 else 0.0
+    """k_rsa_pow against the SIMD issue port (VALU + MFMA issue): algorithmic issue
+    slots per launch (n_grants x 16 x 3,175) / kernel time vs 3.93e13 slots/s.
+    Also: the VALU-resident MACs alone, the int8 MFMA rate, and the CIOS-equivalent
+    work (SURVEY §8d, 132,096 MAC/grant) against the VALU-only peak the previous
+    Montgomery kernel was bound by."""
+    t = pow_ms / 1e3 if pow_ms > 0 else float("inf")
+    slots = n_grants * POW_SQR * POW_ISSUE_SLOTS
+    achieved = slots / t
+    cios = n_grants * MAC_POW_PER_GRANT / t
+    mfma = n_grants * POW_SQR * POW_MFMA_I8_MAC / t
     return {"bound": "valu", "kernel": "k_rsa_pow", "achieved": round(achieved / 1e12, 3),
-            "peak": round(PEAK_MAC_PER_S / 1e12, 3), "unit": "TMAC/s", "frac": round(achieved / PEAK_MAC_PER_S, 4),
-            "traffic": traffic, "algorithmic_mac_per_launch": n_grants * MAC_POW_PER_GRANT,
-            "kernel_ms": round(pow_ms, 4)}
+            "peak": round(PEAK_MAC_PER_S / 1e12, 3), "unit": "T issue-slots/s (v_mad_u64_u32 lane-ops + MFMA issue)",
+            "frac": round(achieved / PEAK_MAC_PER_S, 4), "traffic": traffic,
+            "algorithmic_slots_per_launch": slots, "kernel_ms": round(pow_ms, 4),
+            "valu_mac_tmac_per_s": round(n_grants * POW_SQR * POW_VALU_MAC / t / 1e12, 3),
+            "mfma_i8": {"tmac_per_s": round(mfma / 1e12, 1), "peak_tmac_per_s": INT8_DENSE_PEAK / 1e12,
+                        "frac": round(mfma / INT8_DENSE_PEAK, 4)},
+            "cios_equiv": {"tmac_per_s": round(cios / 1e12, 3),
+                           "vs_valu_only_peak": round(cios / PEAK_MAC_PER_S, 4)}}
 
 
 def main():
@@ -266,7 +291,7 @@ def main():
                                if world > 1 else "dp1",
             },
             "roofline": roofline(N, stage_ms[2], traffic),
-            "path_roofline_frac": round(value / world * MAC_PER_GRANT / PEAK_MAC_PER_S, 4),
+            "path_cios_equiv_vs_valu_peak": round(value / world * MAC_PER_GRANT / PEAK_MAC_PER_S, 4),
             "stage_ms": {"prep_sha256": round(stage_ms[0], 4), "bucket": round(stage_ms[1], 4),
                          "rsa_pow": round(stage_ms[2], 4), "rsa_final": round(stage_ms[3], 4),
                          "tally": round(stage_ms[4], 4)},

@@ -35,10 +35,10 @@ def load_pass(name):
     # runs host-path chunks and the wire path, which launch smaller grids)
     big = collections.defaultdict(int)
     for r in rows:
-        k = r["Kernel_Name"].split("(")[0].replace("mochi::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "")
         big[k] = max(big[k], int(r["Grid_Size"]))
     for r in rows:
-        k = r["Kernel_Name"].split("(")[0].replace("mochi::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "")
         if int(r["Grid_Size"]) != big[k]:
             continue
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--what", default="bench.py --headline-only --steps 2 --warmup 1 (C4: 16M grants, R=4)")
     a = ap.parse_args()
     per = collections.defaultdict(dict)
-    for p in ("sq1", "sq2", "fetch", "write"):
+    for p in ("sq1", "sq2", "sq3", "fetch", "write"):
         for k, d in load_pass(p).items():
             per[k].update(d)
     out = {"source": f"rocprofv3 --pmc, scripts/pmc.sh ({a.what}); values are per dispatch of the largest grid "
@@ -73,6 +73,9 @@ def main():
         if "SQC_ICACHE_HITS" in d:
             tot = d["SQC_ICACHE_HITS"] + d.get("SQC_ICACHE_MISSES", 0) + d.get("SQC_ICACHE_MISSES_DUPLICATE", 0)
             e["icache_miss_rate"] = (d.get("SQC_ICACHE_MISSES", 0) + d.get("SQC_ICACHE_MISSES_DUPLICATE", 0)) / tot
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
+            # MFMA busy cycles summed over the 1,024 SIMDs vs the kernel's GPU cycles
+            e["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (d["GRBM_GUI_ACTIVE"] / 8)
         if "SQ_INSTS_VALU" in d and "SQ_INSTS_VALU_INT64" in d:
             e["valu_int64_share"] = d["SQ_INSTS_VALU_INT64"] / d["SQ_INSTS_VALU"]
         out["kernels"][k] = e

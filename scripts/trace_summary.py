@@ -25,7 +25,7 @@ a = ap.parse_args()
 f = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)[0]
 d = collections.defaultdict(list)
 for r in csv.DictReader(open(f)):
-    name = r["Kernel_Name"].split("(")[0].replace("mochi::", "").replace("(anonymous namespace)::", "")
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "")
     d[(name, int(r["Grid_Size_X"]))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
 out = {}
 for (k, g), v in sorted(d.items(), key=lambda x: -sum(x[1])):
