@@ -57,6 +57,25 @@ def main():
         torch.cuda.synchronize()
         times.append(ev[0].elapsed_time(ev[1]))
     ms = sorted(times)[2]
+    if os.environ.get("FOLD_STAMPS"):
+        lib.fold_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        torch.cuda.synchronize()
+        lib.fold_stamps(None, 1)
+        ev[0].record()
+        lib.fold_pow(x.data_ptr(), w.data_ptr(), c.data_ptr(), z.data_ptr(), N, 16, st)
+        ev[1].record()
+        torch.cuda.synchronize()
+        kms = ev[0].elapsed_time(ev[1])
+        out = np.zeros(6, np.uint64)
+        lib.fold_stamps(out.ctypes.data, 0)
+        waves = int(out[3])
+        per = [int(v) / waves / 16 for v in out[:3]]
+        life = int(out[4]) / waves
+        # 2 waves per SIMD, 1,024 SIMDs: sum of wave lifetimes / 2,048 ~ kernel ticks
+        rate = int(out[4]) / 2048 / (kms / 1e3) / 1e9
+        print(f"stamps per wave-squaring (s_memtime ticks): sqr {per[0]:.0f}  bops {per[1]:.0f}  fold {per[2]:.0f}  "
+              f"waves={waves}  wave lifetime {life:.0f} (loop {16 * sum(per):.0f})  kernel {kms:.3f} ms -> "
+              f"{rate:.3f} G ticks/s if SIMDs always hold 2 waves")
     print(f"N={N} 16 squarings: {ms:.3f} ms/launch  {ms * 1e6 / N:.3f} ns/sig  "
           f"(k_rsa_pow r02: 4.19 ns/sig)  times={['%.3f' % t for t in times]}")
     sys.exit(1 if bad else 0)

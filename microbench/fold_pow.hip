@@ -60,7 +60,19 @@ __device__ __forceinline__ void swap32(int& a, int& b) {
   b = r[1];
 }
 
-__device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restrict__ wl, cptr32 corr) {
+#ifndef STAMPS
+#define STAMPS 0
+#endif
+__device__ __forceinline__ uint64_t stamp() {
+#if STAMPS
+  return __builtin_amdgcn_s_memtime();
+#else
+  return 0;
+#endif
+}
+
+__device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restrict__ wl, cptr32 corr, uint64_t (&acc)[3]) {
+  const uint64_t s0 = stamp();
   uint32_t t[2 * kL];
 #if MF_ONLY
 #pragma unroll
@@ -93,6 +105,8 @@ __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restric
     t[2 * kL - 1] = (uint32_t)carry;
   }
   __builtin_amdgcn_sched_barrier(0);
+  const uint64_t s1 = stamp();
+  acc[0] += s1 - s0;
 #if SQ_ONLY
 #pragma unroll
   for (int q = 0; q < kL; q++) x[q] = t[q] ^ t[q + 74];
@@ -117,6 +131,9 @@ __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restric
     });
   });
   int64_t carry = 0;
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t s2 = stamp();
+  acc[1] += s2 - s1;
   static_for<0, kMT>([&](auto mc) {
     constexpr int mt = decltype(mc)::value;
 #if MT_BARRIER
@@ -161,17 +178,25 @@ __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restric
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_setprio(0);
 #endif
+  __builtin_amdgcn_sched_barrier(0);
+  acc[2] += stamp() - s2;
 }
+
+__device__ uint64_t g_stamps[6];
 
 __global__ __launch_bounds__(512, 1) void k_fold_pow(const uint32_t* __restrict__ xin, const v4i* __restrict__ wimg,
                                                      const uint32_t* __restrict__ corr, uint32_t* __restrict__ zout,
                                                      uint32_t n, int iters) {
   __shared__ v4i w[kMT * kKS * 64];
+#if STAMPS
+  const uint64_t t_begin = stamp();
+#endif
   for (int i = threadIdx.x; i < kMT * kKS * 64; i += blockDim.x) w[i] = wimg[i];
   __syncthreads();
   const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = idx < n;
   uint32_t x[kL];
+  uint64_t acc[3] = {0, 0, 0};
 #pragma unroll
   for (int j = 0; j < kL; j++) x[j] = active ? xin[(size_t)j * n + idx] : 0u;
   const cptr32 c = (cptr32)corr;
@@ -187,15 +212,32 @@ __global__ __launch_bounds__(512, 1) void k_fold_pow(const uint32_t* __restrict_
   for (int it = 0; it < iters; it++) {
     cptr32 ci = c;
     asm volatile("" : "+s"(ci));  // keep the 74 corr loads inside the loop (148 SGPRs if hoisted)
-    fold_sqr(x, w + (threadIdx.x & 63), ci);
+    fold_sqr(x, w + (threadIdx.x & 63), ci, acc);
   }
   if (active) {
 #pragma unroll
     for (int j = 0; j < kL; j++) zout[(size_t)j * n + idx] = x[j];
   }
+#if STAMPS
+  if ((threadIdx.x & 63) == 0) {  // per-phase cycles summed over waves (vector atomics)
+    atomicAdd((unsigned long long*)&g_stamps[0], (unsigned long long)acc[0]);
+    atomicAdd((unsigned long long*)&g_stamps[1], (unsigned long long)acc[1]);
+    atomicAdd((unsigned long long*)&g_stamps[2], (unsigned long long)acc[2]);
+    atomicAdd((unsigned long long*)&g_stamps[3], 1ull);
+    atomicAdd((unsigned long long*)&g_stamps[4], (unsigned long long)(stamp() - t_begin));  // wave lifetime
+  }
+#endif
 }
 
 }  // namespace
+
+extern "C" int fold_stamps(uint64_t* out, int reset) {
+  if (reset) {
+    uint64_t z[6] = {0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 6 * sizeof(uint64_t)) != hipSuccess;
+}
 
 extern "C" int fold_pow(const uint32_t* xin, const void* wimg, const uint32_t* corr, uint32_t* zout, uint32_t n,
                         int iters, void* stream) {

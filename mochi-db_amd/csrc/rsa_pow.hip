@@ -18,8 +18,9 @@
 // operands; one swap per accumulator pair turns the D fragments (half h = rows
 // 4h + 8u + 0..3 = limb 2u + h of the M-tile) back into "own even | own odd".
 //
-// Block = 8 waves = 512 slots of ONE signer (buckets are 512-aligned): the
-// signer's 100 KB image is staged in LDS once per block; 2 waves per SIMD.
+// Group = 512 slots of ONE signer (buckets are 512-aligned), block = 8 waves
+// = one group at a time; the signer's 100 KB image is staged in LDS; 2 waves
+// per SIMD; persistent blocks, one per CU.
 #include "fold.h"
 #include "rsa_common.h"
 
@@ -130,48 +131,75 @@ __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restric
   });
 }
 
+// Persistent: one block per CU walks a contiguous range of 512-slot groups, so
+// the CU never idles between blocks (a block's 8 waves would otherwise all wait
+// for its slowest before the next block could take the LDS) and the signer's
+// image is staged only when the key changes along the range (block-uniform).
 __global__ __launch_bounds__(512, 1) void k_rsa_pow(const uint32_t* __restrict__ perm, uint32_t n_slots,
                                                     const uint8_t* __restrict__ sig,
                                                     const uint16_t* __restrict__ signer,
                                                     const FoldKey* __restrict__ fold, uint32_t* __restrict__ zout) {
   __shared__ v4i w[kFoldImgBytes / 16];
-  const uint32_t base = blockIdx.x * blockDim.x;
-  // buckets are 512-aligned and padded only at their tail: a block whose first
-  // slot is empty is all padding (uniform exit, before the barrier)
-  const uint32_t g_lead = __builtin_amdgcn_readfirstlane(perm[base]);
-  if (g_lead == 0xFFFFFFFFu) return;
-  const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)signer[g_lead]);
-  const v4i* src = (const v4i*)fold[key].img;
-  for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
-  __syncthreads();
-  const uint32_t slot = base + threadIdx.x;
-  const uint32_t g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
-  const bool active = g != 0xFFFFFFFFu;
-  if (__ballot(active) == 0) return;  // no barrier after this point
-  uint32_t x[kL];
-  {
-    uint32_t wd[64];
-    load_sig_words(sig, active ? g : g_lead, wd);  // inactive lanes shadow the lead grant (never stored)
-    words_to_limbs(wd, x);
-  }
-  const cptr c = as_const(fold[key].cadd);
+  const uint32_t n_groups = (n_slots + kBucketAlign - 1) / kBucketAlign;
+  const uint32_t g_begin = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
+  const uint32_t g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
+  uint32_t cur_key = 0xFFFFFFFFu;
+  for (uint32_t grp = g_begin; grp < g_end; grp++) {
+    const uint32_t base = grp * kBucketAlign;
+    // buckets are 512-aligned and padded only at their tail: a group whose
+    // first slot is empty is all padding (every thread reads the same slot)
+    const uint32_t g_lead = __builtin_amdgcn_readfirstlane(perm[base]);
+    if (g_lead == 0xFFFFFFFFu) continue;
+    const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)signer[g_lead]);
+    if (key != cur_key) {  // block-uniform: every wave walks the same groups
+      __syncthreads();     // the old image is no longer read
+      const v4i* src = (const v4i*)fold[key].img;
+      for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
+      __syncthreads();
+      cur_key = key;
+    }
+    const uint32_t slot = base + threadIdx.x;
+    const uint32_t g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
+    const bool active = g != 0xFFFFFFFFu;
+    if (__ballot(active) == 0) continue;  // this wave's quarter of the group is padding
+    uint32_t x[kL];
+    {
+      uint32_t wd[64];
+      load_sig_words(sig, active ? g : g_lead, wd);  // inactive lanes shadow the lead grant (never stored)
+      words_to_limbs(wd, x);
+    }
+    const cptr c = as_const(fold[key].cadd);
 #pragma unroll 1
-  for (int it = 0; it < 16; it++) {
-    cptr ci = c;
-    asm volatile("" : "+s"(ci));  // keep the 74 cadd loads inside the loop (SGPR pressure if hoisted)
-    fold_sqr(x, w + (threadIdx.x & 63), ci);
-  }
-  if (active) {
+    for (int it = 0; it < 16; it++) {
+      cptr ci = c;
+      asm volatile("" : "+s"(ci));  // keep the 74 cadd loads inside the loop (SGPR pressure if hoisted)
+      fold_sqr(x, w + (threadIdx.x & 63), ci);
+    }
+    if (active) {
 #pragma unroll
-    for (int j = 0; j < kL; j++) zout[(size_t)j * n_slots + slot] = x[j];
+      for (int j = 0; j < kL; j++) zout[(size_t)j * n_slots + slot] = x[j];
+    }
   }
 }
 
 }  // namespace
 
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_rsa_pow, dim3((a.n_slots + kBucketAlign - 1) / kBucketAlign), dim3(kBucketAlign), 0, st, a.perm,
-                     a.n_slots, a.sig, a.signer, a.fold, a.xbuf);
+  // one persistent block per CU (the 100 KB image allows one block per CU)
+  static int n_cu[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev >= 0 && dev < 64 && n_cu[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n_cu[dev] = v;
+  }
+  const uint32_t cus = dev >= 0 && dev < 64 ? (uint32_t)n_cu[dev] : 256u;
+  const uint32_t groups = (a.n_slots + kBucketAlign - 1) / kBucketAlign;
+  const uint32_t blocks = groups < cus ? groups : cus;
+  if (blocks)
+    hipLaunchKernelGGL(k_rsa_pow, dim3(blocks), dim3(kBucketAlign), 0, st, a.perm, a.n_slots, a.sig, a.signer, a.fold,
+                       a.xbuf);
 }
 
 }  // namespace mochi
