@@ -402,8 +402,9 @@ enum mochi_msg_status {
    * MOCHI_UNDECIDED: writeCertificate or transaction given more than once; a
    * map entry whose MultiGrant or Grant value is given more than once; a Grant
    * whose bytes are not the canonical encoding Grant.toByteArray() would give
-   * (MochiProtocol.java:7556-7574); more than 32 MultiGrants, 64 grants per
-   * MultiGrant or 64 operations */
+   * (MochiProtocol.java:7556-7574); more than 32 certificate entries, or 64
+   * grants or 64 grantSignatures entries in a decoded MultiGrant (counted on the
+   * wire, repeated keys included), or more than 64 operations */
   MOCHI_MSG_FALLBACK = 2,
   /* op_flags_off gives a different operation count than the message holds */
   MOCHI_MSG_OPS_MISMATCH = 3,

@@ -21,6 +21,7 @@
 #include "../../include/mochi_hip.h"
 #include "kernels.h"
 #include "mont.h"
+#include "w2.h"
 #include "w2_host.h"
 
 namespace {
@@ -94,6 +95,20 @@ struct PinnedBuf {
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---- host-side key precompute (OpenSSL BN, setup only) --------------------
+
+// Cpad = EMSA-PKCS1-v1_5 encoding (RFC 8017 §9.2) of SHA-256 with an all-zero
+// digest: 00 01 FF..FF 00 || DigestInfo(SHA-256) || 32 zero bytes.
+void pkcs1_cpad(uint8_t cpad[256]) {
+  static const uint8_t kDigestInfo[19] = {0x30, 0x31, 0x30, 0x0d, 0x06, 0x09, 0x60, 0x86, 0x48, 0x01,
+                                          0x65, 0x03, 0x04, 0x02, 0x01, 0x05, 0x00, 0x04, 0x20};
+  memset(cpad, 0xFF, 256);
+  cpad[0] = 0x00;
+  cpad[1] = 0x01;
+  cpad[256 - 32 - 19 - 1] = 0x00;
+  memcpy(cpad + 256 - 32 - 19, kDigestInfo, 19);
+  memset(cpad + 256 - 32, 0, 32);
+}
+
 int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
   using namespace mochi;
   memset(e, 0, sizeof *e);
@@ -120,16 +135,8 @@ int make_key_entry(const uint8_t* n_be, mochi::KeyEntry* e) {
   //   kfix = R^2 mod n                           (k_rsa_raw: MontMul(MontMul(z, K), s) = s^65537)
   //   q    = R^-1 mod n                          (k_rsa_final: MontMul(z, s) = s^65537 * q)
   //   a2   = (Cpad * q mod n) + 2n               (k_rsa_final: target EM*q = Cpad*q + H*q)
-  // Cpad = EMSA-PKCS1-v1_5 encoding (RFC 8017 §9.2) of SHA-256 with an all-zero digest.
   uint8_t cpad[256];
-  memset(cpad, 0xFF, sizeof cpad);
-  static const uint8_t kDigestInfo[19] = {0x30, 0x31, 0x30, 0x0d, 0x06, 0x09, 0x60, 0x86, 0x48, 0x01,
-                                          0x65, 0x03, 0x04, 0x02, 0x01, 0x05, 0x00, 0x04, 0x20};
-  cpad[0] = 0x00;
-  cpad[1] = 0x01;
-  cpad[256 - 32 - 19 - 1] = 0x00;
-  memcpy(cpad + 256 - 32 - 19, kDigestInfo, 19);
-  memset(cpad + 256 - 32, 0, 32);
+  pkcs1_cpad(cpad);
   BN_CTX* ctx = BN_CTX_new();
   BIGNUM *n = BN_bin2bn(n_be, 256, nullptr), *r = BN_new(), *k = BN_new(), *ex = BN_new(), *t = BN_new(),
          *q = BN_new(), *a2 = BN_new(), *cp = BN_bin2bn(cpad, 256, nullptr), *n2 = BN_new();
@@ -184,15 +191,23 @@ int make_fold_key(const uint8_t* n_be, mochi::FoldKey* f) {
     }
     ok = ok && carry == 0;
   }
-  // cadd = 128 * sum R_{j,b} as 74 limbs of 28 bits
-  ok = ok && BN_lshift(sum, sum, 7) && BN_num_bits(sum) <= kLimbBits * kFoldLimbs &&
-       BN_bn2lebinpad(sum, le, sizeof le) == (int)sizeof le;
-  for (int q = 0; q < kFoldLimbs && ok; q++) {
-    const int bit = q * kLimbBits, by = bit >> 3;
-    uint64_t w = 0;
-    for (int b = 0; b < 5 && by + b < (int)sizeof le; b++) w |= (uint64_t)le[by + b] << (8 * b);
-    f->cadd[q] = (uint32_t)(w >> (bit & 7)) & kLimbMask;
-  }
+  // cadd = 128 * sum R_{j,b} and cnc = cadd + n - Cpad (k_rsa_final) as 74 limbs of 28 bits
+  auto limbs = [&](const BIGNUM* v, uint32_t* out) {
+    if (BN_num_bits(v) > kLimbBits * kFoldLimbs || BN_bn2lebinpad(v, le, sizeof le) != (int)sizeof le) return 0;
+    for (int q = 0; q < kFoldLimbs; q++) {
+      const int bit = q * kLimbBits, by = bit >> 3;
+      uint64_t w = 0;
+      for (int b = 0; b < 5 && by + b < (int)sizeof le; b++) w |= (uint64_t)le[by + b] << (8 * b);
+      out[q] = (uint32_t)(w >> (bit & 7)) & kLimbMask;
+    }
+    return 1;
+  };
+  uint8_t cpad[256];
+  pkcs1_cpad(cpad);
+  BIGNUM* cp = BN_bin2bn(cpad, 256, nullptr);
+  ok = ok && cp && BN_lshift(sum, sum, 7) && limbs(sum, f->cadd);
+  ok = ok && BN_add(sum, sum, n) && BN_sub(sum, sum, cp) && !BN_is_negative(sum) && limbs(sum, f->cnc);
+  BN_free(cp);
   BN_free(n);
   BN_free(r);
   BN_free(sum);
@@ -793,8 +808,9 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
 // Decode on the device (w2_decode.hip), then the ordinary verify path over the
 // decoded batch, then the per-message status fix-up.  All pointers device.
 // Decode, phase 1 (w2_decode.hip): validate + count + CSR scans for the M
-// messages of `w`.  cnt: 6*(M+1) device words (counts and CSR offsets of this
-// batch, so a pipelined caller can count chunk j+1 while chunk j verifies);
+// messages of `w`.  cnt: mochi::w2_scratch_words(M) device words (counts, CSR
+// offsets and the level-by-level decode state of this batch, so a pipelined
+// caller can count chunk j+1 while chunk j verifies);
 // the totals (N, O, n_mgs) land in tot_host (pinned) once ev_tot completes.
 int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_t* cnt, uint32_t* tot_host,
              hipEvent_t ev_tot, hipStream_t st, mochi::W2Args* a) {
@@ -824,6 +840,9 @@ int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_
   a->cert_grant_off = cnt + 3 * m1;
   a->cert_op_off = cnt + 4 * m1;
   a->cert_mg_off = cnt + 5 * m1;
+  a->cnt_ce = cnt + 6 * m1;
+  a->ce = cnt + (size_t)mochi::kW2MsgArrays * m1;
+  a->ce_cap = mochi::kW2MaxCertEntries * (uint32_t)m1;
   a->status = status;
   a->scan_temp = c->w2_scan.p;
   a->scan_temp_bytes = c->w2_scan.cap;
@@ -921,7 +940,7 @@ int run_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const mochi_par
   const uint32_t M = w->n_msgs;
   if (c->n_ids != c->n_keys) return fail(MOCHI_EINVAL, "server ids not set (mochi_ctx_set_server_ids)");
   int rc;
-  if ((rc = c->w2_cnt.ensure(4 * 6 * ((size_t)M + 1))) || (rc = c->w2_tot.ensure(16)) ||
+  if ((rc = c->w2_cnt.ensure(4 * mochi::w2_scratch_words(M))) || (rc = c->w2_tot.ensure(16)) ||
       (!status && (rc = c->w2_status.ensure(M ? M : 1))))
     return rc;
   HIP_TRY(scratch_acquire(c, st));
@@ -1303,7 +1322,7 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
       in_total = align_up(in_total + seg_bytes(k, i), 256);
     }
     k.cnt = cnt_total;
-    cnt_total += 6 * ((size_t)(k.m1 - k.m0) + 1);
+    cnt_total += mochi::w2_scratch_words(k.m1 - k.m0);
   }
   const size_t nbits = ((size_t)M + 31) / 32 * 4;
   size_t out_total = 0;

@@ -31,7 +31,10 @@ struct FoldKey {
   // the -128 bias of every t_hi byte removes 128 * R_{j,b} per K slot: cadd =
   // 128 * sum R_{j,b} (< 2^2064), added back once as 74 normalised limbs
   uint32_t cadd[kFoldLimbs];
-  uint8_t pad[1024 - kFoldLimbs * 4];
+  // k_rsa_final's constant: cadd + n - Cpad (Cpad = the EMSA-PKCS1-v1_5
+  // encoding with a zero digest), so its fold yields x + n - EM + H directly
+  uint32_t cnc[kFoldLimbs];
+  uint8_t pad[1024 - 2 * kFoldLimbs * 4];
 };
 static_assert(sizeof(FoldKey) == kFoldImgBytes + 1024, "FoldKey layout");
 

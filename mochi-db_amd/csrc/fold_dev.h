@@ -1,0 +1,191 @@
+// fold_dev.h — the modular fold on the matrix cores, shared by k_rsa_pow
+// (rsa_pow.hip: 16 squarings) and k_rsa_final (rsa_final.hip: the multiply
+// by s and the EMSA check).  Layout and bounds: fold.h.
+//
+// Given a 148-limb t (radix 2^28, t < 2^4144), fold_reduce writes the 74
+// normalised limbs of
+//     x = t_lo + sum_{j<75, b<4} byte_b(t_{73+j}) * R_{j,b} + cadd - h
+// where t_lo = limbs 0..72, cadd is a per-key 74-limb constant (k_rsa_pow:
+// the -128 bias correction; k_rsa_final: that plus n - Cpad) and h (k_rsa_final
+// only) a 10-limb value subtracted in the low limbs.  The sum is
+// v_mfma_i32_32x32x32_i8: 10 M-tiles x 10 K-steps x 2 N-tiles (the wave's 64
+// signatures; lane l owns signature l).
+//
+// Fragments: a 32x32x32 B fragment gives lane l (half h = l >> 5) the K slots
+// 16h..16h+15 of column l & 31, so one v_permlane32_swap per operand register
+// pair turns "own t_hi limbs 8s+0..3 | 8s+4..7" into the two N-tiles'
+// operands; one swap per accumulator pair turns the D fragments (half h =
+// rows 4h + 8u + 0..3 = limb 2u + h of the M-tile) back into "own even | own
+// odd" limbs.  A fragments are read from LDS (the key's image) one K-step ahead.
+#pragma once
+#include "fold.h"
+#include "mont.h"
+
+namespace mochi {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void swap32(int& a, int& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+
+// d = a * b + c, signed 32 x 32 + 64 (one v_mad_i64_i32; hipcc otherwise
+// sign-extends, shifts and adds in four instructions)
+__device__ __forceinline__ int64_t mad_i64(int32_t a, int32_t b, int64_t c) {
+  int64_t d;
+  uint64_t cc;
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+
+constexpr int kHL = 10;  // a SHA-256 digest in radix 2^28
+
+// global-address-space byte pointer (keeps global_load/store with an SGPR
+// base + VGPR offset where an asm barrier would otherwise erase the space)
+typedef __attribute__((address_space(1))) char gchar;
+typedef __attribute__((address_space(1))) uint32_t guint;
+
+// t_lo held in registers (k_rsa_pow)
+struct TLoRegs {
+  const uint32_t (&t)[2 * kL];
+  template <int MT>
+  __device__ __forceinline__ void load() {}
+  template <int Q>
+  __device__ __forceinline__ uint32_t get() const { return t[Q]; }
+};
+
+// t_lo parked in memory, limb-major with stride `stride` words (k_rsa_final:
+// frees 73 registers during the product); an M-tile's 8 limbs are loaded
+// before its MFMAs, which cover the latency
+struct TLoMem {
+  const gchar* base;  // wave-uniform
+  size_t stride;     // bytes per limb (wave-uniform)
+  uint32_t off;      // the lane's byte offset
+  uint32_t buf[8];
+  template <int MT>
+  __device__ __forceinline__ void load() {
+    static_for<0, 8>([&](auto rc) {
+      constexpr int q = 8 * MT + decltype(rc)::value;
+      if constexpr (q < kFoldF) {
+        const gchar* b = base;
+        asm volatile("" : "+s"(b));  // recomputed per limb: 73 limb bases would sit in SGPRs and spill
+        buf[q & 7] = *(const guint*)(b + (size_t)q * stride + off);
+      }
+    });
+  }
+  template <int Q>
+  __device__ __forceinline__ uint32_t get() const { return buf[Q & 7]; }
+};
+
+template <bool SUB_H, typename TLo>
+__device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_t (&x)[kL],
+                                            const v4i* __restrict__ wl, cptr cadd, const uint32_t* hl, TLo& tlo) {
+  // ---- B operands: t_hi bytes biased to signed (b - 128), split over the halves ----
+  v4i b0[kFoldKS], b1[kFoldKS];
+  static_for<0, kFoldKS>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<0, 4>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int jp = 8 * s + i, jq = 8 * s + 4 + i;
+      int p = (int)0x80808080u, q = (int)0x80808080u;
+      if constexpr (jp < kFoldNH) p = (int)(t[kFoldF + jp] ^ 0x80808080u);
+      if constexpr (jq < kFoldNH) q = (int)(t[kFoldF + jq] ^ 0x80808080u);
+      swap32(p, q);  // p: N-tile 0 (signatures 0..31), q: N-tile 1 (32..63)
+      b0[s][i] = p;
+      b1[s][i] = q;
+    });
+  });
+  // ---- x = t_lo + fold(t_hi) + cadd (- h), M-tile by M-tile, carries low to high ----
+  int64_t carry = 0;
+  static_for<0, kFoldMT>([&](auto mc) {
+    constexpr int mt = decltype(mc)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    tlo.template load<mt>();
+    v16i d0 = {}, d1 = {};
+    v4i a = wl[(mt * kFoldKS) * 64];
+    static_for<0, kFoldKS>([&](auto sc) {  // one K-step of weights in flight
+      constexpr int s = decltype(sc)::value;
+      v4i an = a;
+      if constexpr (s + 1 < kFoldKS) an = wl[(mt * kFoldKS + s + 1) * 64];
+      d0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      a = an;
+    });
+    static_for<0, 16>([&](auto vc) {
+      constexpr int v = decltype(vc)::value;
+      int e = d0[v], o = d1[v];
+      swap32(e, o);  // e: own even limbs, o: own odd limbs
+      d0[v] = e;
+      d1[v] = o;
+    });
+    static_for<0, 8>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      constexpr int q = 8 * mt + r, u = r >> 1;
+      if constexpr (q < kL) {
+        const v16i& d = (r & 1) ? d1 : d0;
+        // limb q = c0 + 2^8 c1 + 2^16 (c2 + 2^8 c3) + t_lo + cadd (- h) + carry;
+        // the first terms of p stay in int32 (|c0 + 2^8 c1| < 1.27e9, t_lo, cadd
+        // and h < 2^28), h * 2^16 + p + carry is two v_mad_i64_i32
+        int p = d[4 * u] + (d[4 * u + 1] << 8);
+        if constexpr (q < kFoldF) p += (int)tlo.template get<q>();
+        p += (int)cadd[q];
+        if constexpr (SUB_H && q < kHL) p -= (int)hl[q];
+        const int h = d[4 * u + 2] + (d[4 * u + 3] << 8);
+        const int64_t v = mad_i64(h, 65536, mad_i64(p, 1, carry));
+        x[q] = (uint32_t)v & kLimbMask;
+        carry = v >> kLimbBits;
+      }
+    });
+  });
+}
+
+// Persistent walk over 512-slot groups of one signer (buckets are 512-aligned):
+// block b takes a contiguous range of groups; fn(base, key) runs per non-empty
+// group after the signer's fold image is staged in `w` (restaged only when the
+// key changes along the range — block-uniform).
+template <typename F>
+__device__ __forceinline__ void for_groups(const uint32_t* __restrict__ perm, uint32_t n_slots,
+                                           const uint16_t* __restrict__ signer, const FoldKey* __restrict__ fold,
+                                           v4i* w, F&& fn) {
+  const uint32_t n_groups = (n_slots + kBucketAlign - 1) / kBucketAlign;
+  const uint32_t g_begin = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
+  const uint32_t g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
+  uint32_t cur_key = 0xFFFFFFFFu;
+  for (uint32_t grp = g_begin; grp < g_end; grp++) {
+    const uint32_t base = grp * kBucketAlign;
+    // buckets are 512-aligned and padded only at their tail: a group whose
+    // first slot is empty is all padding (every thread reads the same slot)
+    const uint32_t g_lead = __builtin_amdgcn_readfirstlane(perm[base]);
+    if (g_lead == 0xFFFFFFFFu) continue;
+    const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)signer[g_lead]);
+    if (key != cur_key) {
+      __syncthreads();  // the old image is no longer read
+      const v4i* src = (const v4i*)fold[key].img;
+      for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
+      __syncthreads();
+      cur_key = key;
+    }
+    fn(base, key, g_lead);
+  }
+}
+
+// one persistent 512-thread block per CU (the 100 KB image allows one per CU)
+inline uint32_t fold_grid(uint32_t n_slots) {
+  static int n_cu[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev >= 0 && dev < 64 && n_cu[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n_cu[dev] = v;
+  }
+  const uint32_t cus = dev >= 0 && dev < 64 ? (uint32_t)n_cu[dev] : 256u;
+  const uint32_t groups = (n_slots + kBucketAlign - 1) / kBucketAlign;
+  return groups < cus ? groups : cus;
+}
+
+}  // namespace mochi

@@ -1,0 +1,67 @@
+// w2.h — launch interface between the C-ABI layer (capi.cpp) and the
+// Write2ToServer wire decoder (w2_decode.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mochi {
+
+// Write2ToServer wire decode (w2_decode.hip).  Device pointers.
+struct W2Args {
+  // input messages
+  const uint8_t* wire;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  uint32_t M;
+  const uint32_t* flags_off;  // [M+1] or null
+  const uint8_t* flags_in;
+  const int64_t* ots_in;      // aligned with flags_in, or null
+  const uint8_t* ids;         // server-id table
+  const uint32_t* id_off;
+  uint32_t n_ids;
+  // scratch / outputs
+  uint32_t* cnt_g;  // [M+1]
+  uint32_t* cnt_o;  // [M+1]
+  uint32_t* cnt_m;  // [M+1] MultiGrants
+  // level-by-level decode: cnt_ce, ce_base, st_bits, wc_off, wc_len, tx_off,
+  // tx_len ([M+1] each, contiguous from cnt_ce) and the certificate-entry list
+  // (7 arrays of ce_cap words)
+  uint32_t* cnt_ce;
+  uint32_t* ce;
+  uint32_t ce_cap;
+  uint8_t* status;  // [M]
+  void* scan_temp;
+  size_t scan_temp_bytes;
+  uint32_t* cert_grant_off;  // [M+1]
+  uint32_t* cert_op_off;     // [M+1]
+  uint32_t* cert_mg_off;     // [M+1]
+  uint32_t N;          // decoded grant total (emit)
+  uint64_t* sig_src;   // [N] wire offset of each signature (emit -> k_w2_sig)
+  uint64_t* grant_off;
+  uint32_t* grant_len;
+  uint8_t* sig;
+  uint16_t* signer;
+  uint8_t* grant_key;
+  uint8_t* op_key;
+  uint8_t* op_flags;
+  int64_t* op_object_ts;
+  uint64_t* op_key_off;
+  uint32_t* op_key_len;
+  uint32_t* mg_grant_off;    // [n_mgs+1]
+};
+// Device words of one decode's per-batch scratch: 13 arrays of M+1 (counts,
+// CSR offsets, level-1 state) + the certificate-entry list (at most
+// kW2MaxCertEntries per message on the fast path, 7 words each).
+constexpr uint32_t kW2MaxCertEntries = 32;
+constexpr int kW2MsgArrays = 13;
+inline size_t w2_scratch_words(uint32_t M) {
+  return (size_t)kW2MsgArrays * ((size_t)M + 1) + 7 * (size_t)kW2MaxCertEntries * ((size_t)M + 1);
+}
+hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
+hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans
+hipError_t launch_w2_emit(const W2Args& a, hipStream_t stream);
+hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reason, uint8_t* fail_op,
+                           uint8_t* op_decision, uint32_t* op_g0, int64_t* op_ts, hipStream_t stream);
+
+}  // namespace mochi

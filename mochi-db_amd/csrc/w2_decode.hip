@@ -1,15 +1,20 @@
 // w2_decode.hip — Write2ToServer wire messages -> the SoA certificate batch,
 // on the device (one lane per message).
 //
-//   k_w2_valid  validate the whole message the way protobuf-java's parser
-//               would (any malformation -> MOCHI_MSG_MALFORMED)
-//   k_w2_count  apply the fast-path limits (MOCHI_MSG_FALLBACK) and count the
-//               grants and operations a valid message contributes
-//   (scan)      hipcub exclusive sums -> cert_grant_off / cert_op_off
-//   k_w2_emit   re-walk the message and write grant offsets (zero copy into
-//               the wire blob), signatures, signers, key slots, ops
-//   k_w2_fixup  after the verify path: MALFORMED / FALLBACK / OPS_MISMATCH
-//               messages get their reason code and no accept bit
+//   k_w2_msg      level 1, lane = message: top level, operations, the
+//                 WriteCertificate's entry framing and keys; messages outside
+//                 the level-by-level shape are validated whole here
+//   (scan)        certificate-entry offsets
+//   k_w2_entries  the certificate entries into a compact list
+//   k_w2_mg       level 2, lane = certificate entry: validate the MultiGrant,
+//                 resolve map order, count + canonical-check decoded grants
+//   k_w2_final    per message: status and decoded counts; (scans) CSR offsets
+//   k_w2_emit_mg  lane = certificate entry: grant offsets (zero copy into the
+//                 wire blob), signers, key slots, MultiGrant CSR
+//   k_w2_ops      lane = message: operations
+//   k_w2_sig      signatures gathered 16 lanes per grant (coalesced)
+//   k_w2_fixup    after the verify path: MALFORMED / FALLBACK / OPS_MISMATCH
+//                 messages get their reason code and no accept bit
 //
 // Semantics (restated from protobuf-java 3.16.3, pinned by
 // tests/golden/write2_vectors.json and oracle/mochi_oracle.c):
@@ -29,14 +34,14 @@
 #include <hipcub/hipcub.hpp>
 
 #include "../../include/mochi_hip.h"
-#include "kernels.h"
 #include "proto_dev.h"
+#include "w2.h"
 
 namespace mochi {
 namespace {
 
-constexpr uint32_t kMaxMG = 32;           // MultiGrants per certificate (fast path)
-constexpr uint32_t kMaxGrantsPerMG = 64;  // grants per MultiGrant (fast path)
+constexpr uint32_t kMaxMG = kW2MaxCertEntries;  // certificate entries per message (fast path)
+constexpr uint32_t kMaxGrantsPerMG = 64;  // grants entries per decoded MultiGrant (fast path)
 constexpr uint32_t kMaxOps = MOCHI_MAX_OPS_PER_CERT;
 
 struct Fld {
@@ -397,8 +402,7 @@ __device__ bool grant_canonical(ByteReader& r, uint32_t off, uint32_t len) {
   return true;
 }
 
-// Decode one valid message.  COUNT: returns status and counts.  EMIT: writes
-// outputs at g_base / o_base.  Mirrors oracle/mochi_oracle.c decode_one.
+// Decoder outputs (the SoA batch).  Mirrors oracle/mochi_oracle.c decode_one.
 struct W2Out {
   uint64_t* sig_src;  // wire offset of each grant's 256-byte signature, ~0 = none
   uint64_t* grant_off;
@@ -414,216 +418,409 @@ struct W2Out {
   uint32_t* mg_grant_off;
 };
 
-template <bool EMIT>
-__device__ uint32_t decode_msg(ByteReader& r, uint64_t msg_off, const uint8_t* __restrict__ ids,
-                               const uint32_t* __restrict__ id_off, uint32_t n_ids, uint32_t& n_grants,
-                               uint32_t& n_ops, uint32_t& n_mgs, uint32_t g_base, uint32_t o_base, uint32_t m_base,
-                               const uint8_t* flags_in, const int64_t* ots_in, const W2Out& out) {
-  uint32_t wc_off = 0, wc_len = 0, tx_off = 0, tx_len = 0, n_wc = 0, n_tx = 0;
-  {
-    uint32_t pos = 0;
-    Fld f;
+// Per-message decode state (W2Args::cnt_ce onwards; cnt_o is W2Args::cnt_o).
+struct W2Msg {
+  uint32_t *cnt_ce, *ce_base, *st_bits, *wc_off, *wc_len, *tx_off, *tx_len, *cnt_o;
+};
+
+// ---- level by level ------------------------------------------------------------
+// A Write2ToServer message is decoded in two levels, so no lane walks a whole
+// ~2.9 KB message with dependent loads:
+//   level 1, lane = message: the top level, every Operation, and the
+//     WriteCertificate's entries (framing, key UTF-8, value count) -- not the
+//     MultiGrant values;
+//   level 2, lane = certificate entry (one MultiGrant): validates the MultiGrant
+//     value (its grants, Grant values, signatures, strings), resolves the
+//     LinkedHashMap order against its sibling entries and, for the entry that
+//     holds a key's final value, counts the distinct grants and checks them
+//     canonical; the emit kernel later writes that MultiGrant's grants.
+// Messages outside this shape (writeCertificate / transaction repeated, > 32
+// certificate entries, an entry carrying two values, > 64 operations) are
+// validated whole by their level-1 lane (valid_write2) and leave the fast path
+// (MOCHI_MSG_FALLBACK, or MALFORMED).  Status bits per message: level-2 lanes
+// OR theirs in; MALFORMED dominates FALLBACK.
+constexpr uint32_t kStMal = 1u, kStFb = 2u;
+constexpr uint32_t kMaxSigEntries = 64;  // grantSignatures entries per decoded MultiGrant (fast path)
+
+__device__ __noinline__ bool valid_write2_whole(const uint8_t* base, uint32_t len) {
+  ByteReader r;
+  r.init(base, len);
+  return valid_write2(r);
+}
+
+// Level 1 for one message; returns status bits.  nce = certificate entries,
+// nops = operations (both 0 when the message left the fast path).
+__device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint32_t& wc_off, uint32_t& wc_len,
+                              uint32_t& tx_off, uint32_t& tx_len) {
+  uint32_t n_wc = 0, n_tx = 0;
+  bool whole = false;
+  nce = nops = 0;
+  uint32_t pos = 0;
+  Fld f;
+  int rc;
 #pragma unroll 1
-    while (next_fld(r, pos, r.len, f) > 0) {
-      if (f.wt != 2) continue;
-      if (f.field == 1) {
-        wc_off = f.off;
-        wc_len = f.len;
-        n_wc++;
-      } else if (f.field == 2) {
-        tx_off = f.off;
-        tx_len = f.len;
-        n_tx++;
+  while (!whole && (rc = next_fld(r, pos, r.len, f)) > 0) {
+    if (f.wt != 2) continue;
+    if (f.field == 1) {
+      if (++n_wc > 1) {
+        whole = true;
+        break;
       }
-    }
-  }
-  if (n_wc > 1 || n_tx > 1) return MOCHI_MSG_FALLBACK;
-  // operations: key slot = index of the first op naming the same operand1
-  uint32_t no = 0;
-  {
-    uint32_t pos = tx_off, end = tx_off + tx_len;
-    Fld f;
+      wc_off = f.off;
+      wc_len = f.len;
+      uint32_t p2 = f.off, e2 = f.off + f.len;
+      Fld g;
+      int rc2;
 #pragma unroll 1
-    while (next_fld(r, pos, end, f) > 0) {
-      if (f.field != 1 || f.wt != 2) continue;
-      if (no == kMaxOps) return MOCHI_MSG_FALLBACK;
-      if (EMIT) {
-        uint32_t ko, kl;
-        last_string(r, f.off, f.len, 2, ko, kl);
-        uint32_t slot = no, j = 0, p2 = tx_off;
-        Fld g;
-#pragma unroll 1
-        while (j < no && next_fld(r, p2, end, g) > 0) {
-          if (g.field != 1 || g.wt != 2) continue;
-          uint32_t jo, jl;
-          last_string(r, g.off, g.len, 2, jo, jl);
-          if (key_eq(r, jo, jl, ko, kl)) {
-            slot = out.op_key[o_base + j];
-            break;
-          }
-          j++;
-        }
-        // Operation.action (enum, proto3 open): anything but WRITE = 2 / DELETE = 1
-        // fails applyOperation / readOperation (InMemoryDataStore.java:529, :562);
-        // an empty operand1 is never write-locked (:339-358)
-        const int32_t action = (int32_t)(uint32_t)last_varint(r, f.off, f.len, 1);
-        const uint32_t notw = (action != 1 && action != 2) || kl == 0 ? MOCHI_OP_NOT_WRITE : 0;
-        out.op_key[o_base + no] = (uint8_t)slot;
-        out.op_flags[o_base + no] =
-            (uint8_t)((flags_in ? flags_in[no] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC)) | notw);
-        out.op_object_ts[o_base + no] = ots_in ? ots_in[no] : 0;
-        out.op_key_off[o_base + no] = msg_off + ko;
-        out.op_key_len[o_base + no] = kl;
-      }
-      no++;
-    }
-  }
-  n_ops = no;
-  // certificate entries -> MultiGrants -> grants
-  uint32_t n_mg = 0, ng = 0;
-  uint32_t status = MOCHI_MSG_OK;
-  const bool ok = for_map(r, wc_off, wc_len, 1, [&](const Entry&, const Entry& mgv) -> bool {
-    if (++n_mg > kMaxMG) return false;
-    if (EMIT) out.mg_grant_off[m_base + n_mg - 1] = g_base + ng;  // this MultiGrant's first grant
-    const uint32_t mo = mgv.voff, ml = mgv.vlen;
-    uint16_t signer = 0xFFFF;
-    if (EMIT) {
-      uint32_t so, sl;
-      last_string(r, mo, ml, 4, so, sl);  // MultiGrant.serverId
-#pragma unroll 1
-      for (uint32_t k = 0; k < n_ids; k++)
-        if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) {
-          signer = (uint16_t)k;
+      while ((rc2 = next_fld(r, p2, e2, g)) > 0) {
+        if (g.field != 1 || g.wt != 2) continue;
+        if (++nce > kMaxMG) {
+          whole = true;
           break;
         }
+        uint32_t p3 = g.off, e3 = g.off + g.len, nval = 0;
+        Fld h;
+        int rc3;
+#pragma unroll 1
+        while ((rc3 = next_fld(r, p3, e3, h)) > 0) {
+          if (h.wt != 2) continue;
+          if (h.field == 1 && !valid_utf8(r, h.off, h.len)) return kStMal;
+          if (h.field == 2) nval++;
+        }
+        if (rc3 < 0) return kStMal;
+        if (nval > 1) {
+          whole = true;
+          break;
+        }
+      }
+      if (!whole && rc2 < 0) return kStMal;
+    } else if (f.field == 2) {
+      if (++n_tx > 1) {
+        whole = true;
+        break;
+      }
+      tx_off = f.off;
+      tx_len = f.len;
+      uint32_t p2 = f.off, e2 = f.off + f.len;
+      Fld g;
+      int rc2;
+#pragma unroll 1
+      while ((rc2 = next_fld(r, p2, e2, g)) > 0) {
+        if (g.field != 1 || g.wt != 2) continue;
+        if (++nops > kMaxOps) {
+          whole = true;
+          break;
+        }
+        if (!valid_operation(r, g.off, g.len)) return kStMal;
+      }
+      if (!whole && rc2 < 0) return kStMal;
     }
-    uint32_t n_g = 0;
-    return for_map(r, mo, ml, 1, [&](const Entry& ge, const Entry& gv) -> bool {
-      if (++n_g > kMaxGrantsPerMG) return false;
-      if (!EMIT) {
-        if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
-        ng++;
-        return true;
-      }
-      const uint32_t g = g_base + ng++;
-      out.grant_off[g] = msg_off + gv.voff;
-      out.grant_len[g] = gv.vlen;
-      out.signer[g] = signer;
-      // grantSignatures[key]: the last entry with this key, its (last) value
-      uint32_t s_off = 0, s_len = 0;
-      bool have = false;
-      {
-        uint32_t pos = mo, end = mo + ml;
-        Fld f;
+  }
+  if (whole) {
+    nce = nops = 0;
+    return valid_write2_whole(r.base, r.len) ? kStFb : kStMal;
+  }
+  return rc < 0 ? kStMal : 0u;
+}
+
+// Validate a MultiGrant value (valid_multigrant) and count its grants /
+// grantSignatures entries on the wire.
+__device__ bool valid_mg_count(ByteReader& r, uint32_t off, uint32_t len, uint32_t& nge, uint32_t& nse) {
+  uint32_t pos = off, end = off + len;
+  Fld f;
+  int rc;
+  nge = nse = 0;
 #pragma unroll 1
-        while (next_fld(r, pos, end, f) > 0) {
-          if (f.field != 5 || f.wt != 2) continue;
-          Entry se;
-          read_entry(r, f.off, f.len, se);
-          if (key_eq(r, se.koff, se.klen, ge.koff, ge.klen)) {
-            have = true;
-            s_off = se.voff;
-            s_len = se.vlen;
-          }
+  while ((rc = next_fld(r, pos, end, f)) > 0) {
+    if (f.wt != 2) continue;
+    if (f.field == 1) {
+      nge++;
+      if (!valid_leaf_entry(r, f.off, f.len, 1)) return false;
+    } else if (f.field >= 2 && f.field <= 4) {
+      if (!valid_utf8(r, f.off, f.len)) return false;
+    } else if (f.field == 5) {
+      nse++;
+      if (!valid_leaf_entry(r, f.off, f.len, 0)) return false;
+    }
+  }
+  return rc == 0;
+}
+
+// Certificate entries (compact, in wire order per message): message index,
+// key and value slices (message-relative), the index of the entry holding the
+// key's final value (~0 unless this entry is the key's first), and the number
+// of distinct grants of a final-value entry.
+struct CE {
+  uint32_t *msg, *koff, *klen, *voff, *vlen, *last, *ng;
+};
+__host__ __device__ inline CE ce_view(uint32_t* p, uint32_t cap) {
+  return CE{p, p + (size_t)cap, p + 2 * (size_t)cap, p + 3 * (size_t)cap, p + 4 * (size_t)cap, p + 5 * (size_t)cap,
+            p + 6 * (size_t)cap};
+}
+
+// The grants of one decoded MultiGrant value [mo, mo+ml), written from g.
+__device__ void emit_mg(ByteReader& r, uint64_t msg_off, uint32_t mo, uint32_t ml, uint32_t tx_off, uint32_t tx_len,
+                        const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids, uint32_t g,
+                        const W2Out& out) {
+  uint16_t signer = 0xFFFF;
+  {
+    uint32_t so, sl;
+    last_string(r, mo, ml, 4, so, sl);  // MultiGrant.serverId
+#pragma unroll 1
+    for (uint32_t k = 0; k < n_ids; k++)
+      if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) {
+        signer = (uint16_t)k;
+        break;
+      }
+  }
+  for_map(r, mo, ml, 1, [&](const Entry& ge, const Entry& gv) -> bool {
+    out.grant_off[g] = msg_off + gv.voff;
+    out.grant_len[g] = gv.vlen;
+    out.signer[g] = signer;
+    // grantSignatures[key]: the last entry with this key, its (last) value
+    uint32_t s_off = 0, s_len = 0;
+    bool have = false;
+    {
+      uint32_t pos = mo, end = mo + ml;
+      Fld f;
+#pragma unroll 1
+      while (next_fld(r, pos, end, f) > 0) {
+        if (f.field != 5 || f.wt != 2) continue;
+        Entry se;
+        read_entry(r, f.off, f.len, se);
+        if (key_eq(r, se.koff, se.klen, ge.koff, ge.klen)) {
+          have = true;
+          s_off = se.voff;
+          s_len = se.vlen;
         }
       }
-      // the 256 signature bytes are gathered by k_w2_sig (coalesced, 16 lanes per grant)
-      out.sig_src[g] = have && s_len == MOCHI_RSA_BYTES ? msg_off + s_off : ~0ull;
-      // key slot of the first op naming this grant's key
-      uint8_t key = 0xFF;
-      {
-        uint32_t pos = tx_off, end = tx_off + tx_len, j = 0;
-        Fld f;
+    }
+    // the 256 signature bytes are gathered by k_w2_sig (coalesced, 16 lanes per grant)
+    out.sig_src[g] = have && s_len == MOCHI_RSA_BYTES ? msg_off + s_off : ~0ull;
+    // key slot = index of the first op naming this grant's key (that op's own slot)
+    uint8_t key = 0xFF;
+    {
+      uint32_t pos = tx_off, end = tx_off + tx_len, j = 0;
+      Fld f;
 #pragma unroll 1
-        while (next_fld(r, pos, end, f) > 0) {
-          if (f.field != 1 || f.wt != 2) continue;
-          uint32_t ko, kl;
-          last_string(r, f.off, f.len, 2, ko, kl);
-          if (key_eq(r, ko, kl, ge.koff, ge.klen)) {
-            key = out.op_key[o_base + j];
-            break;
-          }
-          j++;
+      while (next_fld(r, pos, end, f) > 0) {
+        if (f.field != 1 || f.wt != 2) continue;
+        uint32_t ko, kl;
+        last_string(r, f.off, f.len, 2, ko, kl);
+        if (key_eq(r, ko, kl, ge.koff, ge.klen)) {
+          key = (uint8_t)j;
+          break;
         }
+        j++;
       }
-      out.grant_key[g] = key;
-      return true;
-    });
+    }
+    out.grant_key[g] = key;
+    g++;
+    return true;
   });
-  if (!ok) status = MOCHI_MSG_FALLBACK;
-  n_grants = ng;
-  n_mgs = n_mg;
-  return status;
 }
 
-// Validation and counting are two kernels, not one: each walk is a chain of
-// dependent loads (latency-bound, lane = message), and latency hiding needs
-// every wave of the grid resident at once.  Fused the walk took 155 VGPRs
-// (3 waves/SIMD: a 250k-message grid ran in 1.3 rounds, 1.60 ms); split, the
-// count walk takes 81 and the validation walk is held to 128 (4 waves/SIMD, a
-// few spills) -- 0.64 + 0.69 ms, vs 0.94 ms for validation at 155 VGPRs.
-// valid[m] is parked in the cert_op_off array, which the exclusive scan
-// overwrites only afterwards.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_w2_valid(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
-                                                  const uint32_t* __restrict__ mlen, uint32_t M,
-                                                  uint32_t* __restrict__ valid) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  ByteReader r;
-  r.init(wire + moff[m], mlen[m]);
-  valid[m] = valid_write2(r) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(256) void k_w2_count(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
-                                                  const uint32_t* __restrict__ mlen, uint32_t M,
-                                                  const uint32_t* __restrict__ flags_off,
-                                                  const uint32_t* __restrict__ valid,
-                                                  uint32_t* __restrict__ cnt_g, uint32_t* __restrict__ cnt_o,
-                                                  uint32_t* __restrict__ cnt_m, uint8_t* __restrict__ status) {
+// Level 1.  cnt_o[m] = operations on the wire (k_w2_final turns it into the
+// decoded count).  Element M of cnt_ce is the scan's extra element.
+__global__ __launch_bounds__(256) void k_w2_msg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                                const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m > M) return;
-  if (m == M) {  // the scan's extra element: totals land at [M]
-    cnt_g[M] = 0;
-    cnt_o[M] = 0;
-    cnt_m[M] = 0;
+  if (m == M) {
+    s.cnt_ce[M] = 0;
     return;
   }
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
-  uint32_t ng = 0, no = 0, nm = 0, st;
-  if (!valid[m]) {
-    st = MOCHI_MSG_MALFORMED;
-  } else {
-    W2Out none{};
-    st = decode_msg<false>(r, moff[m], nullptr, nullptr, 0, ng, no, nm, 0, 0, 0, nullptr, nullptr, none);
-    if (st == MOCHI_MSG_OK && flags_off && flags_off[m + 1] - flags_off[m] != no) st = MOCHI_MSG_OPS_MISMATCH;
+  uint32_t nce, nops, wo = 0, wl = 0, to = 0, tl = 0;
+  const uint32_t bits = msg_level(r, nce, nops, wo, wl, to, tl);
+  if (bits) nce = nops = 0;
+  s.cnt_ce[m] = nce;
+  s.cnt_o[m] = nops;
+  s.st_bits[m] = bits;
+  s.wc_off[m] = wo;
+  s.wc_len[m] = wl;
+  s.tx_off[m] = to;
+  s.tx_len[m] = tl;
+}
+
+// Level 1, second walk: the certificate entries into the compact list.
+__global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                                    const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M || s.cnt_ce[m] == 0) return;
+  ByteReader r;
+  r.init(wire + moff[m], mlen[m]);
+  uint32_t e = s.ce_base[m], pos = s.wc_off[m];
+  const uint32_t end = pos + s.wc_len[m];
+  Fld f;
+#pragma unroll 1
+  while (next_fld(r, pos, end, f) > 0) {
+    if (f.field != 1 || f.wt != 2) continue;
+    Entry x;
+    read_entry(r, f.off, f.len, x);
+    ce.msg[e] = m;
+    ce.koff[e] = x.koff;
+    ce.klen[e] = x.klen;
+    ce.voff[e] = x.voff;
+    ce.vlen[e] = x.vlen;
+    e++;
   }
-  if (st != MOCHI_MSG_OK) ng = no = nm = 0;
+}
+
+// Level 2 (lane = certificate entry; grid-stride over the device-side total).
+__global__ __launch_bounds__(256) void k_w2_mg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                               const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce) {
+  const uint32_t total = s.ce_base[M];
+#pragma unroll 1
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const uint32_t m = ce.msg[e];
+    ByteReader r;
+    r.init(wire + moff[m], mlen[m]);
+    const uint32_t b0 = s.ce_base[m], b1 = s.ce_base[m + 1], ko = ce.koff[e], kl = ce.klen[e];
+    bool first = true;
+    uint32_t last = e;
+#pragma unroll 1
+    for (uint32_t j = b0; j < b1; j++)
+      if (j != e && key_eq(r, ce.koff[j], ce.klen[j], ko, kl)) {
+        if (j < e) first = false;
+        else last = j;
+      }
+    const uint32_t vo = ce.voff[e], vl = ce.vlen[e];
+    uint32_t bits = 0, ng = 0, nge, nse;
+    if (!valid_mg_count(r, vo, vl, nge, nse)) {
+      bits = kStMal;
+    } else if (last == e) {  // this entry's value is the key's final one: it is decoded
+      if (nge > kMaxGrantsPerMG || nse > kMaxSigEntries ||
+          !for_map(r, vo, vl, 1, [&](const Entry&, const Entry& gv) -> bool {
+            if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
+            ng++;
+            return true;
+          }))
+        bits = kStFb;
+    }
+    ce.last[e] = first ? last : ~0u;
+    ce.ng[e] = bits ? 0u : ng;
+    if (bits) atomicOr(s.st_bits + m, bits);
+  }
+}
+
+// Per message: final status and the decoded counts.
+__global__ __launch_bounds__(256) void k_w2_final(uint32_t M, const uint32_t* __restrict__ flags_off, W2Msg s, CE ce,
+                                                  uint32_t* __restrict__ cnt_g, uint32_t* __restrict__ cnt_m,
+                                                  uint8_t* __restrict__ status) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m > M) return;
+  if (m == M) {  // the scans' extra element: totals land at [M]
+    cnt_g[M] = 0;
+    s.cnt_o[M] = 0;
+    cnt_m[M] = 0;
+    return;
+  }
+  const uint32_t bits = s.st_bits[m];
+  uint32_t st = (bits & kStMal) ? MOCHI_MSG_MALFORMED : (bits & kStFb) ? MOCHI_MSG_FALLBACK : MOCHI_MSG_OK;
+  uint32_t no = s.cnt_o[m], ng = 0, nm = 0;
+  if (st == MOCHI_MSG_OK && flags_off && flags_off[m + 1] - flags_off[m] != no) st = MOCHI_MSG_OPS_MISMATCH;
+  if (st == MOCHI_MSG_OK) {
+#pragma unroll 1
+    for (uint32_t j = s.ce_base[m]; j < s.ce_base[m + 1]; j++) {
+      const uint32_t L = ce.last[j];
+      if (L != ~0u) {
+        nm++;
+        ng += ce.ng[L];
+      }
+    }
+  } else {
+    no = 0;
+  }
   cnt_g[m] = ng;
-  cnt_o[m] = no;
+  s.cnt_o[m] = no;
   cnt_m[m] = nm;
   status[m] = (uint8_t)st;
 }
 
-__global__ __launch_bounds__(256) void k_w2_emit(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
-                                                 const uint32_t* __restrict__ mlen, uint32_t M,
-                                                 const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off,
-                                                 uint32_t n_ids, const uint32_t* __restrict__ flags_off,
-                                                 const uint8_t* __restrict__ flags_in,
-                                                 const int64_t* __restrict__ ots_in,
-                                                 const uint32_t* __restrict__ g_base,
-                                                 const uint32_t* __restrict__ o_base,
-                                                 const uint32_t* __restrict__ m_base,
-                                                 const uint8_t* __restrict__ status, W2Out out) {
+// Emit, lane = certificate entry: a key's first entry writes its MultiGrant
+// (the final value's grants) at the position its predecessors leave.
+__global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                                    const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce,
+                                                    const uint8_t* __restrict__ status,
+                                                    const uint32_t* __restrict__ g_base,
+                                                    const uint32_t* __restrict__ m_base, const uint8_t* __restrict__ ids,
+                                                    const uint32_t* __restrict__ id_off, uint32_t n_ids, W2Out out) {
+  const uint32_t total = s.ce_base[M];
+#pragma unroll 1
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const uint32_t L = ce.last[e];
+    if (L == ~0u) continue;
+    const uint32_t m = ce.msg[e];
+    if (status[m] != MOCHI_MSG_OK) continue;
+    uint32_t idx = 0, gb = 0;
+#pragma unroll 1
+    for (uint32_t j = s.ce_base[m]; j < e; j++) {
+      const uint32_t Lj = ce.last[j];
+      if (Lj != ~0u) {
+        idx++;
+        gb += ce.ng[Lj];
+      }
+    }
+    const uint32_t g = g_base[m] + gb;
+    out.mg_grant_off[m_base[m] + idx] = g;  // this MultiGrant's first grant
+    ByteReader r;
+    r.init(wire + moff[m], mlen[m]);
+    emit_mg(r, moff[m], ce.voff[L], ce.vlen[L], s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, g, out);
+  }
+}
+
+// Emit, lane = message: the operations (key slot = index of the first op
+// naming the same operand1) and the MultiGrant CSR terminator.
+__global__ __launch_bounds__(256) void k_w2_ops(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                                const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s,
+                                                const uint8_t* __restrict__ status, const uint32_t* __restrict__ g_base,
+                                                const uint32_t* __restrict__ o_base, const uint32_t* __restrict__ m_base,
+                                                const uint32_t* __restrict__ flags_off,
+                                                const uint8_t* __restrict__ flags_in,
+                                                const int64_t* __restrict__ ots_in, W2Out out) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m == 0) out.mg_grant_off[m_base[M]] = g_base[M];  // CSR terminator: n_mgs -> N
   if (m >= M || status[m] != MOCHI_MSG_OK) return;
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
-  uint32_t ng, no, nm;
-  decode_msg<true>(r, moff[m], ids, id_off, n_ids, ng, no, nm, g_base[m], o_base[m], m_base[m],
-                   flags_off ? flags_in + flags_off[m] : nullptr,
-                   flags_off && ots_in ? ots_in + flags_off[m] : nullptr, out);
+  const uint64_t msg_off = moff[m];
+  const uint32_t ob = o_base[m], tx_off = s.tx_off[m], end = tx_off + s.tx_len[m];
+  const uint8_t* fl = flags_off ? flags_in + flags_off[m] : nullptr;
+  const int64_t* ot = flags_off && ots_in ? ots_in + flags_off[m] : nullptr;
+  uint32_t no = 0, pos = tx_off;
+  Fld f;
+#pragma unroll 1
+  while (next_fld(r, pos, end, f) > 0) {
+    if (f.field != 1 || f.wt != 2) continue;
+    uint32_t ko, kl;
+    last_string(r, f.off, f.len, 2, ko, kl);
+    uint32_t slot = no, j = 0, p2 = tx_off;
+    Fld g;
+#pragma unroll 1
+    while (j < no && next_fld(r, p2, end, g) > 0) {
+      if (g.field != 1 || g.wt != 2) continue;
+      uint32_t jo, jl;
+      last_string(r, g.off, g.len, 2, jo, jl);
+      if (key_eq(r, jo, jl, ko, kl)) {
+        slot = j;
+        break;
+      }
+      j++;
+    }
+    // Operation.action (enum, proto3 open): anything but WRITE = 2 / DELETE = 1
+    // fails applyOperation / readOperation (InMemoryDataStore.java:529, :562);
+    // an empty operand1 is never write-locked (:339-358)
+    const int32_t action = (int32_t)(uint32_t)last_varint(r, f.off, f.len, 1);
+    const uint32_t notw = (action != 1 && action != 2) || kl == 0 ? MOCHI_OP_NOT_WRITE : 0;
+    out.op_key[ob + no] = (uint8_t)slot;
+    out.op_flags[ob + no] = (uint8_t)((fl ? fl[no] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC)) | notw);
+    out.op_object_ts[ob + no] = ot ? ot[no] : 0;
+    out.op_key_off[ob + no] = msg_off + ko;
+    out.op_key_len[ob + no] = kl;
+    no++;
+  }
 }
 
 // sig[g] = wire[sig_src[g] .. +256) (zeros when absent): 16 lanes per grant,
@@ -676,6 +873,18 @@ __global__ __launch_bounds__(256) void k_w2_fixup(const uint8_t* __restrict__ st
 
 inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 
+W2Msg msg_view(const W2Args& a) {
+  const size_t m1 = (size_t)a.M + 1;
+  uint32_t* p = a.cnt_ce;
+  return W2Msg{p, p + m1, p + 2 * m1, p + 3 * m1, p + 4 * m1, p + 5 * m1, p + 6 * m1, a.cnt_o};
+}
+
+// grid of the grid-stride certificate-entry kernels (the entry total is on the device)
+inline uint32_t ce_blocks(const W2Args& a) {
+  const uint32_t b = cdiv((uint64_t)a.ce_cap, 256);
+  return b < 1 ? 1 : b > 2048 ? 2048 : b;
+}
+
 }  // namespace
 
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes) {
@@ -683,14 +892,23 @@ hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes) {
 }
 
 hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
-  if (a.M)
-    hipLaunchKernelGGL(k_w2_valid, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M,
-                       a.cert_op_off);
-  hipLaunchKernelGGL(k_w2_count, dim3(cdiv((uint64_t)a.M + 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len,
-                     a.M, a.flags_off, a.cert_op_off, a.cnt_g, a.cnt_o, a.cnt_m, a.status);
+  const W2Msg s = msg_view(a);
+  const CE ce = ce_view(a.ce, a.ce_cap);
+  const uint32_t gm1 = cdiv((uint64_t)a.M + 1, 256);
+  hipLaunchKernelGGL(k_w2_msg, dim3(gm1), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t tb = a.scan_temp_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, s.cnt_ce, s.ce_base, (int)(a.M + 1), st);
+  if (e != hipSuccess) return e;
+  if (a.M) {
+    hipLaunchKernelGGL(k_w2_entries, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce);
+    hipLaunchKernelGGL(k_w2_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce);
+  }
+  hipLaunchKernelGGL(k_w2_final, dim3(gm1), dim3(256), 0, st, a.M, a.flags_off, s, ce, a.cnt_g, a.cnt_m, a.status);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  tb = a.scan_temp_bytes;
   e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_g, a.cert_grant_off, (int)(a.M + 1), st);
   if (e != hipSuccess) return e;
   tb = a.scan_temp_bytes;
@@ -703,9 +921,13 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
 hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
   W2Out o{a.sig_src, a.grant_off, a.grant_len, a.sig, a.signer, a.grant_key, a.op_key, a.op_flags,
           a.op_object_ts, a.op_key_off, a.op_key_len, a.mg_grant_off};
-  hipLaunchKernelGGL(k_w2_emit, dim3(cdiv(a.M ? a.M : 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M,
-                     a.ids, a.id_off, a.n_ids, a.flags_off, a.flags_in, a.ots_in, a.cert_grant_off, a.cert_op_off,
-                     a.cert_mg_off, a.status, o);
+  const W2Msg s = msg_view(a);
+  const CE ce = ce_view(a.ce, a.ce_cap);
+  if (a.M)
+    hipLaunchKernelGGL(k_w2_emit_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce,
+                       a.status, a.cert_grant_off, a.cert_mg_off, a.ids, a.id_off, a.n_ids, o);
+  hipLaunchKernelGGL(k_w2_ops, dim3(cdiv(a.M ? a.M : 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s,
+                     a.status, a.cert_grant_off, a.cert_op_off, a.cert_mg_off, a.flags_off, a.flags_in, a.ots_in, o);
   if (a.N) hipLaunchKernelGGL(k_w2_sig, dim3(cdiv((uint64_t)a.N * 16, 256)), dim3(256), 0, st, a.wire, a.sig_src, a.N, a.sig);
   return hipGetLastError();
 }

@@ -22,7 +22,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmochi_hip.so")
+# MOCHI_HIP_LIB: an alternative build of the same library (A/B measurements)
+LIB_PATH = os.environ.get("MOCHI_HIP_LIB") or os.path.join(_HERE, "libmochi_hip.so")
 
 RSA_BYTES = 256
 RSA_E = 65537

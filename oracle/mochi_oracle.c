@@ -1155,14 +1155,14 @@ static int decode_one(const uint8_t* m, size_t mlen, uint64_t base, const uint8_
   entry_t* ce;
   const size_t nce = list_entries(m, wc_off, wc_len, 1, &ce);
   int status = MOCHI_MSG_OK;
-  uint32_t n_mg = 0;
   const uint32_t g_start = go->n, mg_start = mo_out->n;
+  /* fast path: at most 32 certificate entries on the wire (duplicates included) */
+  if (nce > W2_MAX_MULTIGRANTS) status = MOCHI_MSG_FALLBACK;
   for (size_t i = 0; i < nce && status == MOCHI_MSG_OK; i++)
     if (ce[i].nval > 1) status = MOCHI_MSG_FALLBACK;
   for (size_t i = 0; i < nce && status == MOCHI_MSG_OK; i++) {
     const long s = map_slot(m, ce, nce, i);
     if (s < 0) continue;
-    if (++n_mg > W2_MAX_MULTIGRANTS) { status = MOCHI_MSG_FALLBACK; break; }
     const size_t mo = ce[s].voff, ml = ce[s].vlen;
     size_t sid_o, sid_l;
     last_string(m, mo, ml, 4, &sid_o, &sid_l); /* MultiGrant.serverId */
@@ -1173,6 +1173,9 @@ static int decode_one(const uint8_t* m, size_t mlen, uint64_t base, const uint8_
     const size_t nge = list_entries(m, mo, ml, 1, &ge);
     const size_t nse = list_entries(m, mo, ml, 5, &se);
     uint32_t n_g = 0;
+    /* fast path: at most 64 grants and 64 grantSignatures entries on the wire
+     * per decoded MultiGrant (duplicates included) */
+    if (nge > W2_MAX_GRANTS_PER_MG || nse > W2_MAX_GRANTS_PER_MG) status = MOCHI_MSG_FALLBACK;
     for (size_t a = 0; a < nge && status == MOCHI_MSG_OK; a++)
       if (ge[a].nval > 1) status = MOCHI_MSG_FALLBACK;
     for (size_t a = 0; a < nge && status == MOCHI_MSG_OK; a++) {

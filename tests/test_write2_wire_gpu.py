@@ -345,6 +345,14 @@ def _fallback_forms(s, c, ids):
         # 29 extra MultiGrants from unknown servers, unsigned, same grant: 33 MultiGrants in all
         "33_multigrants": W.encode_write2(ent + [(f"extra-{i}", W.encode_multigrant([(oid, gb)], f"extra-{i}"))
                                                  for i in range(29)], ops),
+        # 33 certificate entries on the wire, 32 distinct keys (the first entry repeated
+        # last): the fast path counts wire entries, so this leaves it too
+        "33_entries_32_keys": W.encode_write2(ent + [(f"extra-{i}", W.encode_multigrant([(oid, gb)], f"extra-{i}"))
+                                                     for i in range(28)] + [ent[0]], ops),
+        # one MultiGrant repeating its grants / grantSignatures entries 65 times each
+        "65_grant_entries": W.encode_write2(
+            [(ids[r], W.encode_multigrant([(o, gb) for o, gb, _ in it] * 65, ids[r], "cl", "",
+                                          [(o, sg) for o, _, sg in it] * 65)) for r, it in mgs.items()], ops),
         # every grant's fields out of canonical order: the signature covers the canonical
         # re-encoding (Grant.toByteArray()), so it still verifies
         "noncanonical_grants": W.encode_write2(
@@ -362,12 +370,14 @@ def test_wire_fallback_messages_decided_on_host(pool4):
     s = W.make_batch(pool4, 64, first_cert=4242, faults=False)
     ids4 = W.SERVER_IDS[:4]
     msgs, kinds = [], []
+    hashes = []
     for c in range(0, 64, 8):
         for k, m in _fallback_forms(s, c, ids4).items():
             msgs.append(m)
             kinds.append(k)
+            hashes.append(s.batch.expected_hash[c])
     wb = _pack(msgs, pad=1)
-    wb.expected_hash = np.stack([s.batch.expected_hash[c] for c in range(0, 64, 8) for _ in range(5)])
+    wb.expected_hash = np.stack(hashes)
     g, st = ver.verify_write2(wb, 4, True)
     ids, off = W.server_id_table(4)
     o, ost = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)
@@ -376,7 +386,8 @@ def test_wire_fallback_messages_decided_on_host(pool4):
     np.testing.assert_array_equal(g.cert_accept_bits, o.cert_accept_bits)
     kinds = np.array(kinds)
     assert (st[kinds == "canonical"] == mh.MSG_OK).all()
-    assert (st[(kinds == "wc_split") | (kinds == "tx_twice") | (kinds == "33_multigrants")] == mh.MSG_FALLBACK).all()
+    assert (st[np.isin(kinds, ["wc_split", "tx_twice", "33_multigrants", "33_entries_32_keys",
+                               "65_grant_entries"])] == mh.MSG_FALLBACK).all()
     # decided, and like the canonical form: accepted (no faults in this stream)
     assert g.cert_accept.all(), list(zip(kinds, g.cert_reason))
     ver.close()
