@@ -420,7 +420,11 @@ def wire_path(ver, synth, R, strict, dev, stream, args):
         best_dev = min(best_dev, hv.timing_ms["total"] / 1e3)
         host_same &= bool(np.array_equal(hv.cert_reason, host.cert_reason))
     del dwb, out
-    batch_legs = [batcher_leg(ver, wb, synth.batch.cert_grant_off, R, strict, th, host) for th in (2, 20)]
+    ver2 = mh.Verifier(ver.moduli, device=dev)  # a second context: two batches in flight
+    ver2.set_server_ids(W.SERVER_IDS[:R])
+    batch_legs = [batcher_leg(vs, wb, synth.batch.cert_grant_off, R, strict, th, host)
+                  for vs in ([ver], [ver, ver2]) for th in (2, 20)]
+    ver2.close()
     return {"grants_per_s": round(N / t, 1), "ms_per_step": round(t * 1e3, 4), "messages": wb.n_msgs,
             "wire_bytes": int(wb.wire.nbytes), "verdicts_equal_soa_path": same,
             "host_encode_s": round(enc_s, 2),
@@ -433,13 +437,13 @@ def wire_path(ver, synth, R, strict, dev, stream, args):
             "batcher": batch_legs}
 
 
-def batcher_leg(ver, wb, cert_grant_off, R, strict, threads, ref, max_msgs=4096, max_wait_us=100, n_req=20000):
+def batcher_leg(vers, wb, cert_grant_off, R, strict, threads, ref, max_msgs=4096, max_wait_us=100, n_req=20000):
     """The drop-in as a MochiDB server would drive it (C5 proxy): `threads` worker
     threads -- the reference's request pool is core 2 / max 20
     (MochiServer.java:36-40) -- each blocking in mochi_batcher_verify on one
     Write2ToServer body at a time (host bytes in, verdict out); the batcher
-    coalesces whatever is in flight into one GPU call.  Reports per-request
-    latency percentiles and throughput."""
+    coalesces whatever is in flight into one GPU call (one batch in flight per
+    context in `vers`).  Reports per-request latency percentiles and throughput."""
     import threading
 
     import numpy as np
@@ -449,7 +453,7 @@ def batcher_leg(ver, wb, cert_grant_off, R, strict, threads, ref, max_msgs=4096,
     M = min(wb.n_msgs, n_req)
     msgs = [wb.wire[int(wb.msg_off[i]):int(wb.msg_off[i]) + int(wb.msg_len[i])].tobytes() for i in range(M)]
     hashes = [wb.expected_hash[i].tobytes() for i in range(M)]
-    b = mh.Batcher(ver, R, strict, max_msgs=max_msgs, max_wait_us=max_wait_us)
+    b = mh.Batcher(vers, R, strict, max_msgs=max_msgs, max_wait_us=max_wait_us)
     lat = [[] for _ in range(threads)]
     res = [None] * M
 
@@ -474,7 +478,7 @@ def batcher_leg(ver, wb, cert_grant_off, R, strict, threads, ref, max_msgs=4096,
     ls = np.sort(np.concatenate([np.asarray(x) for x in lat])) * 1e6
     reasons = np.array([r[1] for r in res], np.uint8)
     n_grants = int(cert_grant_off[M])
-    return {"threads": threads, "requests": M, "requests_per_s": round(M / wall, 1),
+    return {"threads": threads, "contexts": len(vers), "requests": M, "requests_per_s": round(M / wall, 1),
             "grants_per_s": round(n_grants / wall, 1),
             "latency_us": {"p50": round(float(np.percentile(ls, 50)), 1), "p99": round(float(np.percentile(ls, 99)), 1),
                            "max": round(float(ls[-1]), 1)},

@@ -523,6 +523,11 @@ typedef struct mochi_verdict1 {
  * LOCAL|HAS_SVOC.  The batcher borrows `ctx` (one batcher per context). */
 mochi_batcher* mochi_batcher_create(mochi_ctx* ctx, const mochi_params* params, uint32_t max_msgs,
                                     uint32_t max_wait_us, int with_op_flags);
+/* The same over n_ctx contexts (e.g. two on one GPU): one flusher thread per
+ * context takes the next batch while the others are on the GPU, so n batches
+ * are in flight.  The batcher borrows the contexts. */
+mochi_batcher* mochi_batcher_create_multi(mochi_ctx* const* ctxs, uint32_t n_ctx, const mochi_params* params,
+                                          uint32_t max_msgs, uint32_t max_wait_us, int with_op_flags);
 /* Blocks until this message's verdict is in `out`.  Thread-safe.  Returns the
  * status of the batch call that carried it. */
 int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,

@@ -10,7 +10,8 @@
 // max_msgs pending messages (or whatever is pending once the oldest has waited
 // max_wait_us), verifies them with ONE mochi_verify_write2 call, and wakes each
 // caller with its own verdict.  While a batch is on the GPU the next one
-// accumulates, so the batch size follows the offered load.
+// accumulates, so the batch size follows the offered load; with several
+// contexts (mochi_batcher_create_multi) several batches are in flight at once.
 //
 // Built only on the public C ABI (include/mochi_hip.h).
 #include <chrono>
@@ -37,10 +38,21 @@ struct Request {
   bool done = false;
 };
 
+// One flusher per context: with n contexts, n batches are in flight at once
+// (one assembling/decoding while another's k_rsa_pow runs), so a request that
+// arrives while a batch is on the GPU need not wait for it to come back.
+struct Flusher {
+  mochi_ctx* ctx;
+  std::thread th;
+  // batch assembly buffers (this flusher's thread only)
+  std::vector<uint8_t> wire, flags, hashes, status, reason, fail_op;
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> len, flags_off, accept;
+};
+
 }  // namespace
 
 struct mochi_batcher {
-  mochi_ctx* ctx;
   mochi_params params;
   uint32_t max_msgs, max_wait_us;
   bool with_op_flags;
@@ -49,13 +61,9 @@ struct mochi_batcher {
   std::deque<Request*> q;
   bool stop = false;
   uint64_t n_batches = 0, n_msgs = 0;
-  std::thread flusher;
-  // batch assembly buffers (flusher thread only)
-  std::vector<uint8_t> wire, flags, hashes, status, reason, fail_op;
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> len, flags_off, accept;
+  std::vector<Flusher> fl;
 
-  void run() {
+  void run(Flusher& f) {
     std::vector<Request*> batch;
     for (;;) {
       {
@@ -69,7 +77,7 @@ struct mochi_batcher {
         batch.assign(q.begin(), q.begin() + n);
         q.erase(q.begin(), q.begin() + n);
       }
-      verify(batch);
+      verify(f, batch);
       {
         std::lock_guard<std::mutex> lk(mu);
         for (Request* r : batch) r->done = true;
@@ -80,7 +88,17 @@ struct mochi_batcher {
     }
   }
 
-  void verify(const std::vector<Request*>& batch) {
+  void verify(Flusher& f, const std::vector<Request*>& batch) {
+    auto& wire = f.wire;
+    auto& flags = f.flags;
+    auto& hashes = f.hashes;
+    auto& status = f.status;
+    auto& reason = f.reason;
+    auto& fail_op = f.fail_op;
+    auto& off = f.off;
+    auto& len = f.len;
+    auto& flags_off = f.flags_off;
+    auto& accept = f.accept;
     const uint32_t M = (uint32_t)batch.size();
     size_t total = 0, n_ops = 0;
     const bool any_flags = with_op_flags;
@@ -128,7 +146,7 @@ struct mochi_batcher {
     v.cert_accept_bits = accept.data();
     v.cert_reason = reason.data();
     v.cert_fail_op = fail_op.data();
-    const int rc = mochi_verify_write2(ctx, &w, &params, &v, status.data());
+    const int rc = mochi_verify_write2(f.ctx, &w, &params, &v, status.data());
     for (uint32_t i = 0; i < M; i++) {
       Request* r = batch[i];
       r->rc = rc;
@@ -144,17 +162,28 @@ struct mochi_batcher {
 
 extern "C" {
 
-mochi_batcher* mochi_batcher_create(mochi_ctx* ctx, const mochi_params* params, uint32_t max_msgs,
-                                    uint32_t max_wait_us, int with_op_flags) {
-  if (!ctx || !params || max_msgs == 0) return nullptr;
+mochi_batcher* mochi_batcher_create_multi(mochi_ctx* const* ctxs, uint32_t n_ctx, const mochi_params* params,
+                                          uint32_t max_msgs, uint32_t max_wait_us, int with_op_flags) {
+  if (!ctxs || n_ctx == 0 || !params || max_msgs == 0) return nullptr;
+  for (uint32_t i = 0; i < n_ctx; i++)
+    if (!ctxs[i]) return nullptr;
   mochi_batcher* b = new mochi_batcher();
   b->with_op_flags = with_op_flags != 0;
-  b->ctx = ctx;
   b->params = *params;
   b->max_msgs = max_msgs;
   b->max_wait_us = max_wait_us;
-  b->flusher = std::thread([b] { b->run(); });
+  b->fl.resize(n_ctx);
+  for (uint32_t i = 0; i < n_ctx; i++) b->fl[i].ctx = ctxs[i];
+  for (auto& f : b->fl) {
+    Flusher* fp = &f;
+    f.th = std::thread([b, fp] { b->run(*fp); });
+  }
   return b;
+}
+
+mochi_batcher* mochi_batcher_create(mochi_ctx* ctx, const mochi_params* params, uint32_t max_msgs,
+                                    uint32_t max_wait_us, int with_op_flags) {
+  return mochi_batcher_create_multi(&ctx, 1, params, max_msgs, max_wait_us, with_op_flags);
 }
 
 int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
@@ -193,7 +222,8 @@ void mochi_batcher_destroy(mochi_batcher* b) {
     b->stop = true;
   }
   b->cv_work.notify_all();
-  if (b->flusher.joinable()) b->flusher.join();
+  for (auto& f : b->fl)
+    if (f.th.joinable()) f.th.join();
   delete b;
 }
 

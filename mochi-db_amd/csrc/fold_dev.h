@@ -83,6 +83,10 @@ struct TLoMem {
 template <bool SUB_H, typename TLo>
 __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_t (&x)[kL],
                                             const v4i* __restrict__ wl, cptr cadd, const uint32_t* hl, TLo& tlo) {
+  // tile 0's first A fragment: issued before the B operands are formed (their
+  // ~150 VALU ops cover the LDS latency); every later tile's first fragment is
+  // prefetched by the previous tile's last K-step
+  v4i a = wl[0];
   // ---- B operands: t_hi bytes biased to signed (b - 128), split over the halves ----
   v4i b0[kFoldKS], b1[kFoldKS];
   static_for<0, kFoldKS>([&](auto sc) {
@@ -105,11 +109,10 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
     __builtin_amdgcn_sched_barrier(0);
     tlo.template load<mt>();
     v16i d0 = {}, d1 = {};
-    v4i a = wl[(mt * kFoldKS) * 64];
     static_for<0, kFoldKS>([&](auto sc) {  // one K-step of weights in flight
       constexpr int s = decltype(sc)::value;
       v4i an = a;
-      if constexpr (s + 1 < kFoldKS) an = wl[(mt * kFoldKS + s + 1) * 64];
+      if constexpr (mt * kFoldKS + s + 1 < kFoldMT * kFoldKS) an = wl[(mt * kFoldKS + s + 1) * 64];
       d0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0, 0, 0, 0);
       d1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);

@@ -26,7 +26,7 @@ struct W2Args {
   uint32_t* cnt_m;  // [M+1] MultiGrants
   // level-by-level decode: cnt_ce, ce_base, st_bits, wc_off, wc_len, tx_off,
   // tx_len ([M+1] each, contiguous from cnt_ce) and the certificate-entry list
-  // (7 arrays of ce_cap words)
+  // (11 arrays of ce_cap words)
   uint32_t* cnt_ce;
   uint32_t* ce;
   uint32_t ce_cap;
@@ -52,11 +52,11 @@ struct W2Args {
 };
 // Device words of one decode's per-batch scratch: 13 arrays of M+1 (counts,
 // CSR offsets, level-1 state) + the certificate-entry list (at most
-// kW2MaxCertEntries per message on the fast path, 7 words each).
+// kW2MaxCertEntries per message on the fast path, 11 words each).
 constexpr uint32_t kW2MaxCertEntries = 32;
 constexpr int kW2MsgArrays = 13;
 inline size_t w2_scratch_words(uint32_t M) {
-  return (size_t)kW2MsgArrays * ((size_t)M + 1) + 7 * (size_t)kW2MaxCertEntries * ((size_t)M + 1);
+  return (size_t)kW2MsgArrays * ((size_t)M + 1) + 11 * (size_t)kW2MaxCertEntries * ((size_t)M + 1);
 }
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
 hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans

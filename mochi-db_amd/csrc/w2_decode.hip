@@ -525,7 +525,8 @@ __device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint
 
 // Validate a MultiGrant value (valid_multigrant) and count its grants /
 // grantSignatures entries on the wire.
-__device__ bool valid_mg_count(ByteReader& r, uint32_t off, uint32_t len, uint32_t& nge, uint32_t& nse) {
+__device__ bool valid_mg_count(ByteReader& r, uint32_t off, uint32_t len, uint32_t& nge,
+                                            uint32_t& nse) {
   uint32_t pos = off, end = off + len;
   Fld f;
   int rc;
@@ -546,22 +547,40 @@ __device__ bool valid_mg_count(ByteReader& r, uint32_t off, uint32_t len, uint32
   return rc == 0;
 }
 
+// Distinct grants of a decoded MultiGrant value, each canonical (else false).
+__device__ bool mg_distinct_canonical(ByteReader& r, uint32_t off, uint32_t len, uint32_t& ng) {
+  ng = 0;
+  return for_map(r, off, len, 1, [&](const Entry&, const Entry& gv) -> bool {
+    if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
+    ng++;
+    return true;
+  });
+}
+
 // Certificate entries (compact, in wire order per message): message index,
 // key and value slices (message-relative), the index of the entry holding the
 // key's final value (~0 unless this entry is the key's first), and the number
 // of distinct grants of a final-value entry.
+// A decoded MultiGrant with one distinct grant (the common shape) also leaves
+// its emit record here -- grant value slice, signature offset (message-
+// relative, ~0 = none), signer << 8 | key slot -- written by k_w2_mg while the
+// bytes are hot, so k_w2_emit_mg need not walk it again.
 struct CE {
   uint32_t *msg, *koff, *klen, *voff, *vlen, *last, *ng;
+  uint32_t *r_goff, *r_glen, *r_sig, *r_sk;
 };
 __host__ __device__ inline CE ce_view(uint32_t* p, uint32_t cap) {
-  return CE{p, p + (size_t)cap, p + 2 * (size_t)cap, p + 3 * (size_t)cap, p + 4 * (size_t)cap, p + 5 * (size_t)cap,
-            p + 6 * (size_t)cap};
+  const size_t c = cap;
+  return CE{p, p + c, p + 2 * c, p + 3 * c, p + 4 * c, p + 5 * c, p + 6 * c, p + 7 * c, p + 8 * c, p + 9 * c, p + 10 * c};
 }
 
-// The grants of one decoded MultiGrant value [mo, mo+ml), written from g.
-__device__ void emit_mg(ByteReader& r, uint64_t msg_off, uint32_t mo, uint32_t ml, uint32_t tx_off, uint32_t tx_len,
-                        const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids, uint32_t g,
-                        const W2Out& out) {
+// The distinct grants of one decoded MultiGrant value [mo, mo+ml), in map
+// order: sink(grant value off, len, signer, signature off or ~0, key slot),
+// offsets message-relative.
+template <typename Sink>
+__device__ void walk_mg(ByteReader& r, uint32_t mo, uint32_t ml, uint32_t tx_off, uint32_t tx_len,
+                        const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids,
+                        Sink&& sink) {
   uint16_t signer = 0xFFFF;
   {
     uint32_t so, sl;
@@ -574,9 +593,6 @@ __device__ void emit_mg(ByteReader& r, uint64_t msg_off, uint32_t mo, uint32_t m
       }
   }
   for_map(r, mo, ml, 1, [&](const Entry& ge, const Entry& gv) -> bool {
-    out.grant_off[g] = msg_off + gv.voff;
-    out.grant_len[g] = gv.vlen;
-    out.signer[g] = signer;
     // grantSignatures[key]: the last entry with this key, its (last) value
     uint32_t s_off = 0, s_len = 0;
     bool have = false;
@@ -595,8 +611,6 @@ __device__ void emit_mg(ByteReader& r, uint64_t msg_off, uint32_t mo, uint32_t m
         }
       }
     }
-    // the 256 signature bytes are gathered by k_w2_sig (coalesced, 16 lanes per grant)
-    out.sig_src[g] = have && s_len == MOCHI_RSA_BYTES ? msg_off + s_off : ~0ull;
     // key slot = index of the first op naming this grant's key (that op's own slot)
     uint8_t key = 0xFF;
     {
@@ -614,10 +628,19 @@ __device__ void emit_mg(ByteReader& r, uint64_t msg_off, uint32_t mo, uint32_t m
         j++;
       }
     }
-    out.grant_key[g] = key;
-    g++;
+    sink(gv.voff, gv.vlen, signer, have && s_len == MOCHI_RSA_BYTES ? s_off : ~0u, key);
     return true;
   });
+}
+
+__device__ __forceinline__ void emit_grant(const W2Out& out, uint32_t g, uint64_t msg_off, uint32_t goff, uint32_t glen,
+                                           uint16_t signer, uint32_t sig_off, uint8_t key) {
+  out.grant_off[g] = msg_off + goff;
+  out.grant_len[g] = glen;
+  out.signer[g] = signer;
+  // the 256 signature bytes are gathered by k_w2_sig (coalesced, 16 lanes per grant)
+  out.sig_src[g] = sig_off != ~0u ? msg_off + sig_off : ~0ull;
+  out.grant_key[g] = key;
 }
 
 // Level 1.  cnt_o[m] = operations on the wire (k_w2_final turns it into the
@@ -670,7 +693,9 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
 
 // Level 2 (lane = certificate entry; grid-stride over the device-side total).
 __global__ __launch_bounds__(256) void k_w2_mg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
-                                               const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce) {
+                                               const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce,
+                                               const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off,
+                                               uint32_t n_ids) {
   const uint32_t total = s.ce_base[M];
 #pragma unroll 1
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -691,13 +716,15 @@ __global__ __launch_bounds__(256) void k_w2_mg(const uint8_t* __restrict__ wire,
     if (!valid_mg_count(r, vo, vl, nge, nse)) {
       bits = kStMal;
     } else if (last == e) {  // this entry's value is the key's final one: it is decoded
-      if (nge > kMaxGrantsPerMG || nse > kMaxSigEntries ||
-          !for_map(r, vo, vl, 1, [&](const Entry&, const Entry& gv) -> bool {
-            if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
-            ng++;
-            return true;
-          }))
-        bits = kStFb;
+      if (nge > kMaxGrantsPerMG || nse > kMaxSigEntries || !mg_distinct_canonical(r, vo, vl, ng)) bits = kStFb;
+      else if (ng == 1)
+        walk_mg(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids,
+                [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
+                  ce.r_goff[e] = go;
+                  ce.r_glen[e] = gl;
+                  ce.r_sig[e] = so;
+                  ce.r_sk[e] = (uint32_t)sg << 8 | key;
+                });
     }
     ce.last[e] = first ? last : ~0u;
     ce.ng[e] = bits ? 0u : ng;
@@ -763,11 +790,20 @@ __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ 
         gb += ce.ng[Lj];
       }
     }
-    const uint32_t g = g_base[m] + gb;
+    uint32_t g = g_base[m] + gb;
     out.mg_grant_off[m_base[m] + idx] = g;  // this MultiGrant's first grant
+    const uint64_t mo = moff[m];
+    if (ce.ng[L] == 1) {  // recorded by k_w2_mg
+      const uint32_t sk = ce.r_sk[L];
+      emit_grant(out, g, mo, ce.r_goff[L], ce.r_glen[L], (uint16_t)(sk >> 8), ce.r_sig[L], (uint8_t)sk);
+      continue;
+    }
     ByteReader r;
-    r.init(wire + moff[m], mlen[m]);
-    emit_mg(r, moff[m], ce.voff[L], ce.vlen[L], s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, g, out);
+    r.init(wire + mo, mlen[m]);
+    walk_mg(r, ce.voff[L], ce.vlen[L], s.tx_off[m], s.tx_len[m], ids, id_off, n_ids,
+            [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
+              emit_grant(out, g++, mo, go, gl, sg, so, key);
+            });
   }
 }
 
@@ -903,7 +939,8 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
   if (e != hipSuccess) return e;
   if (a.M) {
     hipLaunchKernelGGL(k_w2_entries, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce);
-    hipLaunchKernelGGL(k_w2_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce);
+    hipLaunchKernelGGL(k_w2_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce, a.ids,
+                       a.id_off, a.n_ids);
   }
   hipLaunchKernelGGL(k_w2_final, dim3(gm1), dim3(256), 0, st, a.M, a.flags_off, s, ce, a.cnt_g, a.cnt_m, a.status);
   e = hipGetLastError();

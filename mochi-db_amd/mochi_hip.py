@@ -189,6 +189,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_signer_set_fault.argtypes = [vp, u32]
     lib.mochi_batcher_create.restype = vp
     lib.mochi_batcher_create.argtypes = [vp, vp, u32, u32, ctypes.c_int]
+    lib.mochi_batcher_create_multi.restype = vp
+    lib.mochi_batcher_create_multi.argtypes = [vp, u32, vp, u32, u32, ctypes.c_int]
     lib.mochi_batcher_verify.argtypes = [vp, vp, u32, vp, u32, vp, vp]
     lib.mochi_batcher_stats.argtypes = [vp, vp, vp]
     lib.mochi_batcher_destroy.argtypes = [vp]
@@ -932,14 +934,18 @@ class Batcher:
     """mochi_batcher: blocking per-request verify, coalesced across calling threads.
     (ctypes drops the GIL during the call, so Python threads block concurrently.)"""
 
-    def __init__(self, verifier: "Verifier", replication_factor: int, strict_gt: bool = True, max_msgs: int = 4096,
+    def __init__(self, verifier, replication_factor: int, strict_gt: bool = True, max_msgs: int = 4096,
                  max_wait_us: int = 200, with_op_flags: bool = False):
-        self.lib = verifier.lib
-        self._ver = verifier
+        # verifier: a Verifier, or a list of them (one flusher, i.e. one batch in
+        # flight, per context: mochi_batcher_create_multi)
+        vers = list(verifier) if isinstance(verifier, (list, tuple)) else [verifier]
+        self.lib = vers[0].lib
+        self._ver = vers
         self._p = params(replication_factor, strict_gt)
         self.with_op_flags = with_op_flags
-        self.h = self.lib.mochi_batcher_create(verifier.ctx, ctypes.addressof(self._p), max_msgs, max_wait_us,
-                                               1 if with_op_flags else 0)
+        self._ctxs = (ctypes.c_void_p * len(vers))(*[v.ctx for v in vers])
+        self.h = self.lib.mochi_batcher_create_multi(self._ctxs, len(vers), ctypes.addressof(self._p), max_msgs,
+                                                     max_wait_us, 1 if with_op_flags else 0)
         if not self.h:
             raise MochiError("mochi_batcher_create failed")
 

@@ -6,4 +6,4 @@ timeout -k 10 300 python -u -m pytest tests/test_write2_wire_gpu.py -x -q -m gpu
 tail -2 $OUT/w2_tests.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/w2_kt" -o run -- python3 "$R/scripts/w2_prof.py" > "$R/$OUT/w2_kt.log" 2>&1 || { tail -20 "$R/$OUT/w2_kt.log"; exit 1; }
-grep -E "k_w2|k_rsa_pow" "$R/$OUT/w2_kt/run_kernel_stats.csv" | cut -d, -f1-4 | sed 's/(.*)"/"/'
+grep -E "k_w2|k_rsa|k_grant|k_tally|k_bucket|Scan" "$R/$OUT/w2_kt/run_kernel_stats.csv" | cut -d, -f1-4 | sed 's/(.*)"/"/'

@@ -248,14 +248,16 @@ def test_wire_edge_shapes(pool4):
     ver.close()
 
 
-@pytest.mark.parametrize("with_flags", [False, True])
-def test_batcher_concurrent_callers(pool4, with_flags):
+@pytest.mark.parametrize("with_flags,n_ctx", [(False, 1), (True, 1), (False, 2)])
+def test_batcher_concurrent_callers(pool4, with_flags, n_ctx):
     """mochi_batcher: 16 threads each block on their own messages; every caller
-    gets exactly the verdict the one-shot batch call gives, and the requests
-    were coalesced into far fewer GPU batches than messages."""
+    gets exactly the verdict the oracle gives, and the requests were coalesced
+    into far fewer GPU batches than messages (n_ctx contexts: that many batches
+    in flight, mochi_batcher_create_multi)."""
     import threading
 
-    ver = _ver(pool4)
+    vers = [_ver(pool4) for _ in range(n_ctx)]
+    ver = vers[0]
     s = W.make_batch(pool4, 1200, first_cert=5000)
     wb = W.encode_wire_batch(s)
     if with_flags:
@@ -263,7 +265,7 @@ def test_batcher_concurrent_callers(pool4, with_flags):
         wb.op_flags[::7] = mh.OP_HAS_SVOC  # some ops not local -> WRONG_SHARD, never checked
     ids, off = W.server_id_table(4)
     ref, ref_st = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)  # the oracle, not the library itself
-    b = mh.Batcher(ver, 4, True, max_msgs=128, max_wait_us=2000, with_op_flags=with_flags)
+    b = mh.Batcher(vers, 4, True, max_msgs=128, max_wait_us=2000, with_op_flags=with_flags)
     M = wb.n_msgs
     res = [None] * M
     msgs = [wb.wire[int(wb.msg_off[i]):int(wb.msg_off[i]) + int(wb.msg_len[i])].tobytes() for i in range(M)]
@@ -286,7 +288,8 @@ def test_batcher_concurrent_callers(pool4, with_flags):
     np.testing.assert_array_equal(acc, ref.cert_accept)
     np.testing.assert_array_equal(np.array([r[1] for r in res], np.uint8), ref.cert_reason)
     np.testing.assert_array_equal(np.array([r[3] for r in res], np.uint8), ref_st)
-    ver.close()
+    for v in vers:
+        v.close()
 
 
 def _fields(b):
