@@ -43,46 +43,14 @@ __device__ __forceinline__ int64_t mad_i64(int32_t a, int32_t b, int64_t c) {
 
 constexpr int kHL = 10;  // a SHA-256 digest in radix 2^28
 
-// global-address-space byte pointer (keeps global_load/store with an SGPR
-// base + VGPR offset where an asm barrier would otherwise erase the space)
+// global-address-space pointers (keep global_load with an SGPR base + VGPR
+// offset where an asm barrier would otherwise erase the address space)
 typedef __attribute__((address_space(1))) char gchar;
 typedef __attribute__((address_space(1))) uint32_t guint;
 
-// t_lo held in registers (k_rsa_pow)
-struct TLoRegs {
-  const uint32_t (&t)[2 * kL];
-  template <int MT>
-  __device__ __forceinline__ void load() {}
-  template <int Q>
-  __device__ __forceinline__ uint32_t get() const { return t[Q]; }
-};
-
-// t_lo parked in memory, limb-major with stride `stride` words (k_rsa_final:
-// frees 73 registers during the product); an M-tile's 8 limbs are loaded
-// before its MFMAs, which cover the latency
-struct TLoMem {
-  const gchar* base;  // wave-uniform
-  size_t stride;     // bytes per limb (wave-uniform)
-  uint32_t off;      // the lane's byte offset
-  uint32_t buf[8];
-  template <int MT>
-  __device__ __forceinline__ void load() {
-    static_for<0, 8>([&](auto rc) {
-      constexpr int q = 8 * MT + decltype(rc)::value;
-      if constexpr (q < kFoldF) {
-        const gchar* b = base;
-        asm volatile("" : "+s"(b));  // recomputed per limb: 73 limb bases would sit in SGPRs and spill
-        buf[q & 7] = *(const guint*)(b + (size_t)q * stride + off);
-      }
-    });
-  }
-  template <int Q>
-  __device__ __forceinline__ uint32_t get() const { return buf[Q & 7]; }
-};
-
-template <bool SUB_H, typename TLo>
+template <bool SUB_H>
 __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_t (&x)[kL],
-                                            const v4i* __restrict__ wl, cptr cadd, const uint32_t* hl, TLo& tlo) {
+                                            const v4i* __restrict__ wl, cptr cadd, const uint32_t* hl) {
   // tile 0's first A fragment: issued before the B operands are formed (their
   // ~150 VALU ops cover the LDS latency); every later tile's first fragment is
   // prefetched by the previous tile's last K-step
@@ -107,7 +75,6 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
   static_for<0, kFoldMT>([&](auto mc) {
     constexpr int mt = decltype(mc)::value;
     __builtin_amdgcn_sched_barrier(0);
-    tlo.template load<mt>();
     v16i d0 = {}, d1 = {};
     static_for<0, kFoldKS>([&](auto sc) {  // one K-step of weights in flight
       constexpr int s = decltype(sc)::value;
@@ -134,7 +101,7 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
         // the first terms of p stay in int32 (|c0 + 2^8 c1| < 1.27e9, t_lo, cadd
         // and h < 2^28), h * 2^16 + p + carry is two v_mad_i64_i32
         int p = d[4 * u] + (d[4 * u + 1] << 8);
-        if constexpr (q < kFoldF) p += (int)tlo.template get<q>();
+        if constexpr (q < kFoldF) p += (int)t[q];
         p += (int)cadd[q];
         if constexpr (SUB_H && q < kHL) p -= (int)hl[q];
         const int h = d[4 * u + 2] + (d[4 * u + 3] << 8);

@@ -20,124 +20,128 @@
 //
 // s < n mirrors OpenSSL's RSA_R_DATA_TOO_LARGE_FOR_MODULUS reject.
 //
-// Grid: like k_rsa_pow — persistent 512-thread blocks over the signer's
-// 512-slot groups, the signer's fold image in LDS.
+// Grid: like k_rsa_pow — persistent blocks over the signer's 512-slot groups,
+// the signer's fold image in LDS — but one wave per SIMD (256 threads, two
+// halves per group): with 512 registers z, s and the 148-limb product stay in
+// registers (at 256 the product's peak would spill).
 #include "fold_dev.h"
 #include "rsa_common.h"
 
 namespace mochi {
 namespace {
 
-__global__ __launch_bounds__(512, 1) void k_rsa_final(const uint32_t* __restrict__ perm, uint32_t n_slots,
-                                                      const uint8_t* __restrict__ sig,
-                                                      const uint16_t* __restrict__ signer,
-                                                      const KeyEntry* __restrict__ keys,
-                                                      const FoldKey* __restrict__ fold,
-                                                      const uint32_t* __restrict__ zin,
-                                                      const uint32_t* __restrict__ digest, uint32_t n_grants,
-                                                      uint8_t* __restrict__ flags) {
-  __shared__ v4i w[kFoldImgBytes / 16];
-  for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
-    const uint32_t slot = base + threadIdx.x;
-    const uint32_t g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
-    const bool active = g != 0xFFFFFFFFu;
-    if (__ballot(active) == 0) return;  // this wave's quarter of the group is padding
-    const uint32_t gg = active ? g : g_lead;  // inactive lanes shadow the lead grant (never stored)
-    const KeyEntry* ke = keys + key;
-    const cptr n = as_const(ke->n);
-    uint32_t sv[kL], x[kL];
-    {
-      uint32_t wd[64];
-      load_sig_words(sig, gg, wd);
-      words_to_limbs(wd, sv);
-    }
-    // s < n on the normalised limbs (borrow chain)
-    int32_t br = 0;
+// One wave's worth of grants: slot = this lane's bucket slot.
+__device__ __forceinline__ void final_slot(uint32_t slot, uint32_t base, uint32_t key, uint32_t g_lead,
+                                           const uint32_t* __restrict__ perm, uint32_t n_slots,
+                                           const uint8_t* __restrict__ sig, const KeyEntry* __restrict__ keys,
+                                           const FoldKey* __restrict__ fold, const uint32_t* __restrict__ zin,
+                                           const uint32_t* __restrict__ digest, uint32_t n_grants,
+                                           uint8_t* __restrict__ flags, const v4i* w) {
+  const uint32_t g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
+  const bool active = g != 0xFFFFFFFFu;
+  if (__ballot(active) == 0) return;  // this wave's part of the group is padding
+  const uint32_t gg = active ? g : g_lead;  // inactive lanes shadow the lead grant (never stored)
+  const KeyEntry* ke = keys + key;
+  const cptr n = as_const(ke->n);
+  uint32_t sv[kL], x[kL];
+  {
+    uint32_t wd[64];
+    load_sig_words(sig, gg, wd);
+    words_to_limbs(wd, sv);
+  }
+  // s < n on the normalised limbs (borrow chain)
+  int32_t br = 0;
 #pragma unroll
-    for (int j = 0; j < kL; j++) br = ((int32_t)sv[j] - (int32_t)n[j] - br) < 0 ? 1 : 0;
-    asm volatile("" : "+v"(br));  // decide here (sunk to its use, it keeps s live through the fold)
-    const bool s_lt_n = br != 0;
-    // z limb j of this slot: a wave-uniform limb base (SGPRs) + the lane's byte
-    // offset (one VGPR), so no 64-bit address per limb stays live.  Every slot
-    // of a non-empty group is < n_slots (buckets end 512-aligned inside it).
-    gchar* const zb = (gchar*)const_cast<uint32_t*>(zin);
+  for (int j = 0; j < kL; j++) br = ((int32_t)sv[j] - (int32_t)n[j] - br) < 0 ? 1 : 0;
+  asm volatile("" : "+v"(br));  // decide here (sunk to its use, it keeps s live through the fold)
+  const bool s_lt_n = br != 0;
+  // z limb j of this slot: a wave-uniform limb base (SGPRs) + the lane's byte
+  // offset (one VGPR), so no 64-bit address per limb stays live.  Every slot
+  // of a non-empty group is < n_slots (buckets end 512-aligned inside it).
+  {
+    const gchar* zp = (const gchar*)zin;
     const uint32_t zoff = slot * 4u;
     const size_t zstride = (size_t)n_slots * 4u;
-    {
-      const gchar* zp = zb;
 #pragma unroll
-      for (int j = 0; j < kL; j++) {
-        x[j] = *(const guint*)(zp + zoff);
-        zp += zstride;
-        asm volatile("" : "+s"(zp));  // a running pointer: 74 limb bases would sit in SGPRs and spill
-      }
+    for (int j = 0; j < kL; j++) {
+      x[j] = *(const guint*)(zp + zoff);
+      zp += zstride;
+      asm volatile("" : "+s"(zp));  // a running pointer: 74 limb bases would sit in SGPRs and spill
     }
-    // ---- t = z * s: product scanning, two accumulators per column; t_lo is
-    // parked in this slot's z column (z[k] is consumed by column k before
-    // t[k] overwrites it; padding lanes write their own padding slot), freeing
-    // 73 registers for the product's peak ----
-    uint32_t t[2 * kL];
-    {
-      uint64_t carry = 0;
-      gchar* tp = zb;
-      static_for<0, 2 * kL - 1>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        constexpr int lo = k - kL + 1 > 0 ? k - kL + 1 : 0;
-        constexpr int hi = k < kL - 1 ? k : kL - 1;
-        uint64_t a0 = carry, a1 = 0;
-        static_for<lo, hi + 1>([&](auto ic) {
-          constexpr int i = decltype(ic)::value;
-          if constexpr (i & 1) a1 = mad64(x[i], sv[k - i], a1);
-          else a0 = mad64(x[i], sv[k - i], a0);
-        });
-        const uint64_t acc = a0 + a1;
-        if constexpr (k < kFoldF) {
-          *(guint*)(tp + zoff) = (uint32_t)acc & kLimbMask;
-          tp += zstride;
-          asm volatile("" : "+s"(tp));
-        } else {
-          t[k] = (uint32_t)acc & kLimbMask;
-          asm volatile("" : "+v"(t[k]));  // materialise the 28-bit limb
-        }
-        carry = acc >> kLimbBits;
-        __builtin_amdgcn_sched_barrier(0);  // column by column (see fold_sqr)
+  }
+  // ---- t = z * s: product scanning, two accumulators per column ----
+  uint32_t t[2 * kL];
+  {
+    uint64_t carry = 0;
+    static_for<0, 2 * kL - 1>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int lo = k - kL + 1 > 0 ? k - kL + 1 : 0;
+      constexpr int hi = k < kL - 1 ? k : kL - 1;
+      uint64_t a0 = carry, a1 = 0;
+      static_for<lo, hi + 1>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i & 1) a1 = mad64(x[i], sv[k - i], a1);
+        else a0 = mad64(x[i], sv[k - i], a0);
       });
-      t[2 * kL - 1] = (uint32_t)carry;
-    }
-    // digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
-    uint32_t hl[kHL];
-    {
-      uint32_t hw[8];
+      const uint64_t acc = a0 + a1;
+      t[k] = (uint32_t)acc & kLimbMask;
+      asm volatile("" : "+v"(t[k]));  // materialise the 28-bit limb
+      carry = acc >> kLimbBits;
+      __builtin_amdgcn_sched_barrier(0);  // column by column (see fold_sqr)
+    });
+    t[2 * kL - 1] = (uint32_t)carry;
+  }
+  // digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
+  uint32_t hl[kHL];
+  {
+    uint32_t hw[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) hw[i] = digest[(size_t)(7 - i) * n_grants + gg];
+    for (int i = 0; i < 8; i++) hw[i] = digest[(size_t)(7 - i) * n_grants + gg];
 #pragma unroll
-      for (int j = 0; j < kHL; j++) {
-        const int bit = j * kLimbBits, wi = bit >> 5, sh = bit & 31;
-        const uint64_t v = ((uint64_t)(wi + 1 < 8 ? hw[wi + 1] : 0u) << 32) | hw[wi];
-        hl[j] = (uint32_t)(v >> sh) & kLimbMask;
-      }
+    for (int j = 0; j < kHL; j++) {
+      const int bit = j * kLimbBits, wi = bit >> 5, sh = bit & 31;
+      const uint64_t v = ((uint64_t)(wi + 1 < 8 ? hw[wi + 1] : 0u) << 32) | hw[wi];
+      hl[j] = (uint32_t)(v >> sh) & kLimbMask;
     }
-    // ---- D = t_lo + fold(t_hi) + cadd + n - Cpad - H ----
-    TLoMem tlo{zb, zstride, zoff, {}};
-    fold_reduce<true>(t, x, w + (threadIdx.x & 63), as_const(fold[key].cnc), hl, tlo);
-    // ---- D' = (D + m n) / 2^28 == n ? ----
-    cptr nn = n;
-    asm volatile("" : "+s"(nn));  // reload n here (kept from the s < n check it would sit in SGPRs and spill)
-    const uint32_t n0inv = *as_const(&ke->n0inv);
-    const uint32_t m = (x[0] * n0inv) & kLimbMask;
-    uint64_t c = mad64(m, nn[0], x[0]) >> kLimbBits;  // the low 28 bits cancel
-    uint32_t diff = 0;
+  }
+  // ---- D = t_lo + fold(t_hi) + cadd + n - Cpad - H ----
+  fold_reduce<true>(t, x, w + (threadIdx.x & 63), as_const(fold[key].cnc), hl);
+  // ---- D' = (D + m n) / 2^28 == n ? ----
+  cptr nn = n;
+  asm volatile("" : "+s"(nn));  // reload n here (kept from the s < n check it would sit in SGPRs and spill)
+  const uint32_t n0inv = *as_const(&ke->n0inv);
+  const uint32_t m = (x[0] * n0inv) & kLimbMask;
+  uint64_t c = mad64(m, nn[0], x[0]) >> kLimbBits;  // the low 28 bits cancel
+  uint32_t diff = 0;
 #pragma unroll
-    for (int k = 1; k < kL; k++) {
-      const uint64_t acc = mad64(m, nn[k], x[k] + c);
-      diff |= ((uint32_t)acc & kLimbMask) ^ nn[k - 1];
-      c = acc >> kLimbBits;
-    }
-    diff |= c != (uint64_t)nn[kL - 1] ? 1u : 0u;
-    if (active) {
-      const bool ok = s_lt_n && diff == 0;
-      flags[g] = flags[g] | (ok ? MOCHI_GRANT_SIG_OK : 0);
-    }
+  for (int k = 1; k < kL; k++) {
+    const uint64_t acc = mad64(m, nn[k], x[k] + c);
+    diff |= ((uint32_t)acc & kLimbMask) ^ nn[k - 1];
+    c = acc >> kLimbBits;
+  }
+  diff |= c != (uint64_t)nn[kL - 1] ? 1u : 0u;
+  if (active) {
+    const bool ok = s_lt_n && diff == 0;
+    flags[g] = flags[g] | (ok ? MOCHI_GRANT_SIG_OK : 0);
+  }
+}
+
+// 256 threads (one wave per SIMD, 512 registers: z, s and the whole product
+// stay in registers) walk each 512-slot group in two halves.
+__global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict__ perm, uint32_t n_slots,
+                                                       const uint8_t* __restrict__ sig,
+                                                       const uint16_t* __restrict__ signer,
+                                                       const KeyEntry* __restrict__ keys,
+                                                       const FoldKey* __restrict__ fold,
+                                                       const uint32_t* __restrict__ zin,
+                                                       const uint32_t* __restrict__ digest, uint32_t n_grants,
+                                                       uint8_t* __restrict__ flags) {
+  __shared__ v4i w[kFoldImgBytes / 16];
+  for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
+#pragma unroll 1
+    for (uint32_t h = 0; h < kBucketAlign; h += 256)
+      final_slot(base + h + threadIdx.x, base, key, g_lead, perm, n_slots, sig, keys, fold, zin, digest,
+                        n_grants, flags, w);
   });
 }
 
@@ -149,9 +153,9 @@ void launch_rsa_final(const LaunchArgs& a, hipStream_t st) {
     return;
   }
   const uint32_t blocks = fold_grid(a.n_slots);
-  if (blocks)
-    hipLaunchKernelGGL(k_rsa_final, dim3(blocks), dim3(kBucketAlign), 0, st, a.perm, a.n_slots, a.sig, a.signer,
-                       a.keys, a.fold, a.xbuf, a.digest, a.n_grants, a.flags);
+  if (!blocks) return;
+  hipLaunchKernelGGL(k_rsa_final, dim3(blocks), dim3(256), 0, st, a.perm, a.n_slots, a.sig, a.signer, a.keys, a.fold,
+                     a.xbuf, a.digest, a.n_grants, a.flags);
 }
 
 }  // namespace mochi

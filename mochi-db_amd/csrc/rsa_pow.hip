@@ -55,8 +55,7 @@ __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restric
     });
     t[2 * kL - 1] = (uint32_t)carry;
   }
-  TLoRegs tlo{t};
-  fold_reduce<false>(t, x, wl, cadd, nullptr, tlo);
+  fold_reduce<false>(t, x, wl, cadd, nullptr);
 }
 
 // Persistent: one block per CU walks a contiguous range of 512-slot groups, so
