@@ -158,3 +158,34 @@ def test_oracle_ops_mismatch_status():
     wb.op_flags = np.full(3, 3, np.uint8)
     d = O.w2_decode(wb, blob, off)
     assert int(d["msg_status"][0]) == 3
+
+
+def test_oracle_fast_path_counts_wire_entries():
+    """The device fast path bounds its per-lane map resolution by counting entries
+    on the wire, repeated keys included (w2_decode.hip k_w2_msg / k_w2_mg; restated in
+    oracle/mochi_oracle.c decode_one): 32 certificate entries decode, 33 leave the fast
+    path even when two share a key; a decoded MultiGrant with 65 grants or 65
+    grantSignatures entries (one key repeated) leaves it too.  The full decode still
+    yields the LinkedHashMap result for all of them."""
+    ids, off = W.server_id_table(4)
+    gb = W.encode_grant("obj-a", 7, "h" * 128, 1, 1)
+    sig = b"\x01" * 256
+
+    def mg(n_grants=1, n_sigs=1, sid=W.SERVER_IDS[0]):
+        return W.encode_multigrant([("obj-a", gb)] * n_grants, sid, "cl", "", [("obj-a", sig)] * n_sigs)
+
+    ops = [W.encode_operation(2, "obj-a")]
+    cases = {
+        "32_entries": (W.encode_write2([(f"k{i}", mg()) for i in range(32)], ops), 0, 32),
+        "33_entries_32_keys": (W.encode_write2([(f"k{i}", mg()) for i in range(32)] + [("k0", mg())], ops), 2, 32),
+        "64_grant_entries": (W.encode_write2([("k0", mg(n_grants=64))], ops), 0, 1),
+        "65_grant_entries": (W.encode_write2([("k0", mg(n_grants=65))], ops), 2, 1),
+        "65_sig_entries": (W.encode_write2([("k0", mg(n_sigs=65))], ops), 2, 1),
+    }
+    for name, (m, fast, n_mgs_full) in cases.items():
+        d = O.w2_decode(_single(m), ids, off)
+        assert int(d["msg_status"][0]) == fast, name
+        f = O.w2_decode_full(_single(m), ids, off)
+        assert int(f["msg_status"][0]) == 0, name
+        assert int(f["cert_mg_off"][1]) == n_mgs_full, name
+        assert int(f["cert_grant_off"][1]) == n_mgs_full, name  # one distinct grant per MultiGrant
