@@ -156,6 +156,66 @@ __global__ __launch_bounds__(256) void k_mad_u64_sgpr(uint64_t* out, uint32_t se
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+#define SIMPLE64_KERNEL(NAME, ASM)                                                      \
+  __global__ __launch_bounds__(256) void NAME(uint64_t* out, uint32_t seed, int iters) { \
+    uint32_t a = seed * (threadIdx.x + 1);                                              \
+    uint64_t b = ((uint64_t)seed << 32) ^ (threadIdx.x * 0x9E3779B97F4A7C15ull);        \
+    uint64_t acc[kChains];                                                              \
+    _Pragma("unroll") for (int i = 0; i < kChains; i++) acc[i] = (uint64_t)(i + threadIdx.x) << 20; \
+    for (int it = 0; it < iters; it++) {                                                \
+      _Pragma("unroll") for (int u = 0; u < kUnroll; u++)                               \
+      _Pragma("unroll") for (int i = 0; i < kChains; i++)                               \
+        asm volatile(ASM : "+v"(acc[i]) : "v"(a), "v"(b));                              \
+    }                                                                                   \
+    uint64_t s = 0;                                                                     \
+    _Pragma("unroll") for (int i = 0; i < kChains; i++) s ^= acc[i];                    \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                     \
+  }
+
+// the glue of k_rsa_pow's x^2 columns and fold reassembly (rsa_pow.hip, fold_dev.h)
+SIMPLE64_KERNEL(k_lshl_add_u64, "v_lshl_add_u64 %0, %0, 1, %2")
+SIMPLE64_KERNEL(k_lshrrev_b64, "v_lshrrev_b64 %0, 28, %0")
+SIMPLE64_KERNEL(k_ashrrev_i64, "v_ashrrev_i64 %0, 28, %0")
+SIMPLE_KERNEL(k_and, "v_and_b32 %0, %1, %0")
+SIMPLE_KERNEL(k_xor, "v_xor_b32 %0, %1, %0")
+SIMPLE_KERNEL(k_lshl_add_u32, "v_lshl_add_u32 %0, %1, 8, %0")
+
+__global__ __launch_bounds__(256) void k_mad_i64(uint64_t* out, uint32_t seed, int iters) {
+  int32_t a = (int32_t)(seed * (threadIdx.x + 1)), b = (int32_t)(seed ^ (threadIdx.x * 0x9E3779B9u));
+  int64_t acc[kChains];
+#pragma unroll
+  for (int i = 0; i < kChains; i++) acc[i] = (int64_t)(i + threadIdx.x) << 7;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++)
+#pragma unroll
+      for (int i = 0; i < kChains; i++) {
+        uint64_t c;
+        asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(acc[i]), "=s"(c) : "v"(a), "v"(b));
+      }
+  }
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kChains; i++) s ^= acc[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)s;
+}
+
+__global__ __launch_bounds__(256) void k_permlane32_swap(uint64_t* out, uint32_t seed, int iters) {
+  uint32_t x[kChains], y[kChains];
+#pragma unroll
+  for (int i = 0; i < kChains; i++) { x[i] = seed + i + threadIdx.x; y[i] = seed ^ i; }
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++)
+#pragma unroll
+      for (int i = 0; i < kChains; i++) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(x[i]), "+v"(y[i]));
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kChains; i++) s ^= x[i] ^ y[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 typedef void (*kfn)(uint64_t*, uint32_t, int);
 
 static double run(const char* name, kfn f, int insts_per_step, uint64_t* d, int blocks, int iters) {
@@ -213,6 +273,14 @@ int main(int argc, char** argv) {
   run("v_and_or_b32", k_and_or, 1, d, blocks, iters);
   run("v_dot2_u32_u16", k_dot2_u16, 1, d, blocks, iters);
   run("v_fma_f64", k_fma_f64, 1, d, blocks, iters);
+  run("v_lshl_add_u64", k_lshl_add_u64, 1, d, blocks, iters);
+  run("v_lshrrev_b64", k_lshrrev_b64, 1, d, blocks, iters);
+  run("v_ashrrev_i64", k_ashrrev_i64, 1, d, blocks, iters);
+  run("v_mad_i64_i32", k_mad_i64, 1, d, blocks, iters);
+  run("v_and_b32", k_and, 1, d, blocks, iters);
+  run("v_xor_b32", k_xor, 1, d, blocks, iters);
+  run("v_lshl_add_u32", k_lshl_add_u32, 1, d, blocks, iters);
+  run("v_permlane32_swap_b32", k_permlane32_swap, 1, d, blocks, iters);
   CHECK(hipFree(d));
   return 0;
 }

@@ -48,7 +48,8 @@ constexpr int kHL = 10;  // a SHA-256 digest in radix 2^28
 typedef __attribute__((address_space(1))) char gchar;
 typedef __attribute__((address_space(1))) uint32_t guint;
 
-template <bool SUB_H>
+// BIASED: t_hi limbs (t[kFoldF..]) arrive already XOR 0x80808080.
+template <bool SUB_H, bool BIASED = false>
 __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_t (&x)[kL],
                                             const v4i* __restrict__ wl, cptr cadd, const uint32_t* hl) {
   // tile 0's first A fragment: issued before the B operands are formed (their
@@ -63,8 +64,8 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
       constexpr int i = decltype(ic)::value;
       constexpr int jp = 8 * s + i, jq = 8 * s + 4 + i;
       int p = (int)0x80808080u, q = (int)0x80808080u;
-      if constexpr (jp < kFoldNH) p = (int)(t[kFoldF + jp] ^ 0x80808080u);
-      if constexpr (jq < kFoldNH) q = (int)(t[kFoldF + jq] ^ 0x80808080u);
+      if constexpr (jp < kFoldNH) p = (int)(BIASED ? t[kFoldF + jp] : t[kFoldF + jp] ^ 0x80808080u);
+      if constexpr (jq < kFoldNH) q = (int)(BIASED ? t[kFoldF + jq] : t[kFoldF + jq] ^ 0x80808080u);
       swap32(p, q);  // p: N-tile 0 (signatures 0..31), q: N-tile 1 (32..63)
       b0[s][i] = p;
       b1[s][i] = q;

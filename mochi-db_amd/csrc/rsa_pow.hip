@@ -46,16 +46,17 @@ __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restric
       asm("" : "+v"(xs));  // double the column sum once (else hipcc doubles every x_i: extra mads and registers)
       uint64_t acc = carry + (xs << 1);
       if constexpr ((k & 1) == 0) acc = mad64(x[k >> 1], x[k >> 1], acc);
-      t[k] = (uint32_t)acc & kLimbMask;
+      // t_hi limbs leave here already biased for the fold's signed B operand
+      t[k] = k < kFoldF ? (uint32_t)acc & kLimbMask : ((uint32_t)acc & kLimbMask) ^ 0x80808080u;
       asm volatile("" : "+v"(t[k]));  // materialise the 28-bit limb (else the 64-bit column stays live)
       carry = acc >> kLimbBits;
       // column by column: left alone the scheduler hoists later columns' mads
       // and keeps ~40 64-bit column sums live
       __builtin_amdgcn_sched_barrier(0);
     });
-    t[2 * kL - 1] = (uint32_t)carry;
+    t[2 * kL - 1] = (uint32_t)carry ^ 0x80808080u;
   }
-  fold_reduce<false>(t, x, wl, cadd, nullptr);
+  fold_reduce<false, true>(t, x, wl, cadd, nullptr);
 }
 
 // Persistent: one block per CU walks a contiguous range of 512-slot groups, so
