@@ -16,35 +16,28 @@ namespace mochi {
 struct ByteReader {
   const uint8_t* base;  // grant start
   uint32_t len;
-  uint32_t cached_idx;  // aligned 16-byte chunk index (relative to abase) held in `w`
-  uint4 w;
-  uintptr_t abase;      // base rounded down to 16
-  uint32_t shift;       // base & 15
+  uint32_t cached_idx;  // aligned word index (relative to aligned base) held in `w`
+  uint32_t w;
+  uintptr_t abase;      // base rounded down to 4
+  uint32_t shift;       // base & 3
 
   __device__ __forceinline__ void init(const uint8_t* p, uint32_t l) {
     base = p;
     len = l;
-    abase = (uintptr_t)p & ~(uintptr_t)15;
-    shift = (uint32_t)((uintptr_t)p & 15);
+    abase = (uintptr_t)p & ~(uintptr_t)3;
+    shift = (uint32_t)((uintptr_t)p & 3);
     cached_idx = 0xFFFFFFFFu;
-    w = make_uint4(0, 0, 0, 0);
-  }
-  // the 4-byte word holding byte offset a (a = i + shift), from the cached chunk
-  // (a 16-byte aligned chunk that holds an in-bounds byte never leaves the
-  // buffer's pages; one load per 16 bytes walked instead of per 4)
-  __device__ __forceinline__ uint32_t word(uint32_t a) {
-    const uint32_t ci = a >> 4;
-    if (ci != cached_idx) {
-      w = *(const uint4*)(abase + 16 * (uintptr_t)ci);
-      cached_idx = ci;
-    }
-    const uint32_t k = (a >> 2) & 3;
-    return k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
+    w = 0;
   }
   // byte i (i < len)
   __device__ __forceinline__ uint32_t at(uint32_t i) {
     const uint32_t a = i + shift;
-    return (word(a) >> (8 * (a & 3))) & 0xFFu;
+    const uint32_t wi = a >> 2;
+    if (wi != cached_idx) {
+      w = *(const uint32_t*)(abase + 4 * (uintptr_t)wi);  // word holds byte i: in bounds
+      cached_idx = wi;
+    }
+    return (w >> (8 * (a & 3))) & 0xFFu;
   }
 };
 
@@ -90,8 +83,8 @@ __device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
       // ASCII fast path: skip every remaining byte of the cached word when all
       // of them are ASCII and inside the string (keys and the 128-char hex
       // transactionHash are ASCII, so this is 4 bytes per step)
-      const uint32_t a = off + i + r.shift, sub = a & 3, rest = 4 - sub;
-      if (i + rest <= n && ((r.word(a) >> (8 * sub)) & (0x80808080u >> (8 * sub))) == 0) i += rest;
+      const uint32_t sub = (off + i + r.shift) & 3, rest = 4 - sub;
+      if (i + rest <= n && ((r.w >> (8 * sub)) & (0x80808080u >> (8 * sub))) == 0) i += rest;
       else i++;
       continue;
     }
