@@ -424,6 +424,7 @@ def wire_path(ver, synth, R, strict, dev, stream, args):
     ver2.set_server_ids(W.SERVER_IDS[:R])
     batch_legs = [batcher_leg(vs, wb, synth.batch.cert_grant_off, R, strict, th, host)
                   for vs in ([ver], [ver, ver2]) for th in (2, 20)]
+    async_leg = batcher_async_leg([ver, ver2], wb, synth.batch.cert_grant_off, R, strict, host)
     ver2.close()
     return {"grants_per_s": round(N / t, 1), "ms_per_step": round(t * 1e3, 4), "messages": wb.n_msgs,
             "wire_bytes": int(wb.wire.nbytes), "verdicts_equal_soa_path": same,
@@ -434,7 +435,7 @@ def wire_path(ver, synth, R, strict, dev, stream, args):
                                     "verdicts_equal": host_same,
                                     "note": "mochi_verify_write2: pageable wire bytes staged + chunked H2D / decode+"
                                             "verify / D2H pipeline; device-event span, wall includes host staging"},
-            "batcher": batch_legs}
+            "batcher": batch_legs, "batcher_async": async_leg}
 
 
 def batcher_leg(vers, wb, cert_grant_off, R, strict, threads, ref, max_msgs=4096, max_wait_us=100, n_req=20000):
@@ -485,6 +486,61 @@ def batcher_leg(vers, wb, cert_grant_off, R, strict, threads, ref, max_msgs=4096
             "gpu_batches": nb - nb0, "mean_batch_msgs": round((nm - nm0) / max(1, nb - nb0), 2),
             "verdicts_equal_one_shot": bool(np.array_equal(reasons, ref.cert_reason[:M])),
             "max_wait_us": max_wait_us}
+
+
+def batcher_async_leg(vers, wb, cert_grant_off, R, strict, ref, n_req=100000, window=8192, max_msgs=4096,
+                      max_wait_us=200):
+    """The event-loop form (mochi_batcher_submit): one producer thread keeps up to
+    `window` Write2ToServer bodies in flight and each completion callback frees a
+    slot -- how a Netty handler completing futures would drive the library.
+    Reports requests/s, grants/s and submit->callback latency percentiles."""
+    import threading
+
+    import numpy as np
+
+    import mochi_hip as mh
+
+    M = min(wb.n_msgs, n_req)
+    msgs = [wb.wire[int(wb.msg_off[i]):int(wb.msg_off[i]) + int(wb.msg_len[i])].tobytes() for i in range(M)]
+    hashes = [wb.expected_hash[i].tobytes() for i in range(M)]
+    b = mh.Batcher(vers, R, strict, max_msgs=max_msgs, max_wait_us=max_wait_us)
+    slots = threading.Semaphore(window)
+    t_sub = np.zeros(M)
+    lat = np.zeros(M)
+    reasons = np.zeros(M, np.uint8)
+    left = [M]
+    cv = threading.Condition()
+
+    def done_for(i):
+        def done(rc, accepted, reason, fail_op, status):
+            lat[i] = time.perf_counter() - t_sub[i]
+            reasons[i] = reason if rc == mh.OK else 255
+            slots.release()
+            with cv:
+                left[0] -= 1
+                if left[0] == 0:
+                    cv.notify()
+        return done
+
+    nb0, nm0 = b.stats()
+    t0 = time.perf_counter()
+    for i in range(M):
+        slots.acquire()
+        t_sub[i] = time.perf_counter()
+        b.submit(msgs[i], hashes[i], done_for(i))
+    with cv:
+        cv.wait_for(lambda: left[0] == 0, timeout=300)
+    wall = time.perf_counter() - t0
+    nb, nm = b.stats()
+    b.close()
+    ls = np.sort(lat) * 1e6
+    return {"requests": M, "contexts": len(vers), "window": window, "requests_per_s": round(M / wall, 1),
+            "grants_per_s": round(int(cert_grant_off[M]) / wall, 1),
+            "latency_us": {"p50": round(float(np.percentile(ls, 50)), 1),
+                           "p99": round(float(np.percentile(ls, 99)), 1)},
+            "gpu_batches": nb - nb0, "mean_batch_msgs": round((nm - nm0) / max(1, nb - nb0), 1),
+            "verdicts_equal_one_shot": bool(np.array_equal(reasons, ref.cert_reason[:M])),
+            "note": "one Python producer thread (ctypes call + callback per request bound the rate)"}
 
 
 def wire_pipelined(ver, dwb, R, strict, dev, args, N, ref_host):

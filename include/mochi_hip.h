@@ -532,6 +532,15 @@ mochi_batcher* mochi_batcher_create_multi(mochi_ctx* const* ctxs, uint32_t n_ctx
  * status of the batch call that carried it. */
 int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
                          uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict1* out);
+/* Non-blocking form for an event-loop caller (e.g. a Netty handler completing a
+ * future): enqueue one message and return; cb(user, rc, &verdict) runs on a
+ * flusher thread once its batch is verified (rc = the batch call's status).
+ * msg / op_flags / expected_hash must stay valid until the callback.  With
+ * thousands of requests in flight the batches grow to max_msgs, so throughput
+ * follows the bulk wire path instead of 1 / latency per blocked thread. */
+typedef void (*mochi_verdict_cb)(void* user, int rc, const mochi_verdict1* verdict);
+int mochi_batcher_submit(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
+                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict_cb cb, void* user);
 int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs);
 /* Drains pending requests, then stops the flusher. */
 void mochi_batcher_destroy(mochi_batcher* b);

@@ -33,7 +33,9 @@ struct Request {
   uint32_t n_ops;
   const uint8_t* expected_hash;
   std::chrono::steady_clock::time_point t_enq;
-  mochi_verdict1* out;
+  mochi_verdict1* out;  // blocking call: the caller's verdict slot
+  mochi_verdict_cb cb;  // mochi_batcher_submit: completion callback (heap request)
+  void* user;
   int rc = 0;
   bool done = false;
 };
@@ -64,7 +66,7 @@ struct mochi_batcher {
   std::vector<Flusher> fl;
 
   void run(Flusher& f) {
-    std::vector<Request*> batch;
+    std::vector<Request*> batch, owned;
     for (;;) {
       {
         std::unique_lock<std::mutex> lk(mu);
@@ -77,14 +79,22 @@ struct mochi_batcher {
         batch.assign(q.begin(), q.begin() + n);
         q.erase(q.begin(), q.begin() + n);
       }
-      verify(f, batch);
+      verify(f, batch);  // fills the blocking callers' slots, runs the submitters' callbacks
+      // the submitted (heap) requests are freed here; a blocking caller's request
+      // lives on its stack and may be gone the moment it sees `done`, so it is
+      // not touched again after that
+      owned.clear();
+      for (Request* r : batch)
+        if (r->cb) owned.push_back(r);
       {
         std::lock_guard<std::mutex> lk(mu);
-        for (Request* r : batch) r->done = true;
+        for (Request* r : batch)
+          if (!r->cb) r->done = true;
         n_batches++;
         n_msgs += batch.size();
       }
       cv_done.notify_all();
+      for (Request* r : owned) delete r;
     }
   }
 
@@ -150,12 +160,15 @@ struct mochi_batcher {
     for (uint32_t i = 0; i < M; i++) {
       Request* r = batch[i];
       r->rc = rc;
+      mochi_verdict1 v{};
       if (rc == MOCHI_OK) {
-        r->out->accepted = (uint8_t)((accept[i >> 5] >> (i & 31)) & 1u);
-        r->out->reason = reason[i];
-        r->out->fail_op = fail_op[i];
-        r->out->msg_status = status[i];
+        v.accepted = (uint8_t)((accept[i >> 5] >> (i & 31)) & 1u);
+        v.reason = reason[i];
+        v.fail_op = fail_op[i];
+        v.msg_status = status[i];
       }
+      if (r->cb) r->cb(r->user, rc, &v);
+      else if (rc == MOCHI_OK) *r->out = v;
     }
   }
 };
@@ -198,6 +211,8 @@ int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len,
   r.n_ops = n_ops;
   r.expected_hash = expected_hash;
   r.out = out;
+  r.cb = nullptr;
+  r.user = nullptr;
   r.t_enq = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lk(b->mu);
   if (b->stop) return MOCHI_EINVAL;
@@ -205,6 +220,31 @@ int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len,
   if (b->q.size() == 1 || b->q.size() >= b->max_msgs) b->cv_work.notify_one();
   b->cv_done.wait(lk, [&] { return r.done; });
   return r.rc;
+}
+
+int mochi_batcher_submit(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
+                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict_cb cb, void* user) {
+  if (!b || (!msg && msg_len) || !expected_hash || !cb) return MOCHI_EINVAL;
+  if (b->with_op_flags ? (op_flags == nullptr && n_ops != 0) : (op_flags != nullptr || n_ops != 0))
+    return MOCHI_EINVAL;
+  Request* r = new Request();
+  r->msg = msg;
+  r->msg_len = msg_len;
+  r->op_flags = op_flags;
+  r->n_ops = n_ops;
+  r->expected_hash = expected_hash;
+  r->out = nullptr;
+  r->cb = cb;
+  r->user = user;
+  r->t_enq = std::chrono::steady_clock::now();
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->stop) {
+    delete r;
+    return MOCHI_EINVAL;
+  }
+  b->q.push_back(r);
+  if (b->q.size() == 1 || b->q.size() >= b->max_msgs) b->cv_work.notify_one();
+  return MOCHI_OK;
 }
 
 int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs) {

@@ -192,6 +192,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_batcher_create_multi.restype = vp
     lib.mochi_batcher_create_multi.argtypes = [vp, u32, vp, u32, u32, ctypes.c_int]
     lib.mochi_batcher_verify.argtypes = [vp, vp, u32, vp, u32, vp, vp]
+    lib.mochi_batcher_submit.argtypes = [vp, vp, u32, vp, u32, vp, VERDICT_CB, vp]
     lib.mochi_batcher_stats.argtypes = [vp, vp, vp]
     lib.mochi_batcher_destroy.argtypes = [vp]
     lib.mochi_shard_plan.argtypes = [u32, vp, u32, vp]
@@ -930,6 +931,9 @@ class Verdict1_C(ctypes.Structure):
                 ("msg_status", ctypes.c_uint8)]
 
 
+VERDICT_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Verdict1_C))
+
+
 class Batcher:
     """mochi_batcher: blocking per-request verify, coalesced across calling threads.
     (ctypes drops the GIL during the call, so Python threads block concurrently.)"""
@@ -948,6 +952,29 @@ class Batcher:
                                                      max_wait_us, 1 if with_op_flags else 0)
         if not self.h:
             raise MochiError("mochi_batcher_create failed")
+        # mochi_batcher_submit: requests in flight keyed by the callback's user word
+        import itertools
+
+        self._seq = itertools.count(1)
+        self._pending = {}
+        self._cb = VERDICT_CB(self._on_done)
+
+    def _on_done(self, user, rc, v):
+        _, _, _, done = self._pending.pop(user)
+        d = v.contents
+        done(rc, bool(d.accepted), d.reason, d.fail_op, d.msg_status)
+
+    def submit(self, msg: bytes, expected_hash: bytes, done, op_flags: Optional[bytes] = None):
+        """Non-blocking (mochi_batcher_submit): done(rc, accepted, reason, fail_op,
+        msg_status) runs on a flusher thread once the message's batch is verified."""
+        key = next(self._seq)
+        self._pending[key] = (msg, expected_hash, op_flags, done)  # alive until the callback
+        fl = op_flags if op_flags is not None else None
+        rc = self.lib.mochi_batcher_submit(self.h, msg, len(msg), fl, len(fl) if fl else 0, expected_hash, self._cb,
+                                           key)
+        if rc != OK:
+            self._pending.pop(key, None)
+            raise MochiError(f"mochi_batcher_submit rc={rc}")
 
     def verify(self, msg: bytes, expected_hash: bytes, op_flags: Optional[bytes] = None):
         out = Verdict1_C()

@@ -292,6 +292,46 @@ def test_batcher_concurrent_callers(pool4, with_flags, n_ctx):
         v.close()
 
 
+def test_batcher_async_submit(pool4):
+    """mochi_batcher_submit: one producer keeps every message in flight at once
+    (the event-loop form); each completion callback carries the oracle's verdict
+    and the batches grow far beyond what blocked threads would give."""
+    import threading
+
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 1200, first_cert=9100)
+    wb = W.encode_wire_batch(s)
+    ids, off = W.server_id_table(4)
+    ref, ref_st = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)
+    b = mh.Batcher(ver, 4, True, max_msgs=512, max_wait_us=500)
+    M = wb.n_msgs
+    res = [None] * M
+    left = [M]
+    cv = threading.Condition()
+
+    def done_for(i):
+        def done(rc, accepted, reason, fail_op, status):
+            res[i] = (rc, accepted, reason, status)
+            with cv:
+                left[0] -= 1
+                cv.notify()
+        return done
+
+    for i in range(M):
+        msg = wb.wire[int(wb.msg_off[i]):int(wb.msg_off[i]) + int(wb.msg_len[i])].tobytes()
+        b.submit(msg, wb.expected_hash[i].tobytes(), done_for(i))
+    with cv:
+        assert cv.wait_for(lambda: left[0] == 0, timeout=60)
+    nb, nm = b.stats()
+    b.close()
+    assert nm == M and nb <= M // 64
+    assert all(r[0] == mh.OK for r in res)
+    np.testing.assert_array_equal(np.array([r[1] for r in res]), ref.cert_accept)
+    np.testing.assert_array_equal(np.array([r[2] for r in res], np.uint8), ref.cert_reason)
+    np.testing.assert_array_equal(np.array([r[3] for r in res], np.uint8), ref_st)
+    ver.close()
+
+
 def _fields(b):
     """(tag, raw field bytes) of a protobuf message with varint / length-delimited fields."""
     out, i = [], 0
