@@ -86,26 +86,33 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
       __builtin_amdgcn_sched_barrier(0);
       a = an;
     });
-    static_for<0, 16>([&](auto vc) {
-      constexpr int v = decltype(vc)::value;
-      int e = d0[v], o = d1[v];
-      swap32(e, o);  // e: own even limbs, o: own odd limbs
-      d0[v] = e;
-      d1[v] = o;
+    // the two halves of each limb (c0 + 2^8 c1 and c2 + 2^8 c3) in the MFMA's
+    // own layout -- half h of the wave holds limb 2u + h of both N-tiles'
+    // signatures, all four digits in one lane (rows 4h + 8u + 0..3) -- then one
+    // swap per half turns "limb 2u+h of signatures l and l+32" into "limbs 2u
+    // and 2u+1 of my own signature": 8 swaps per tile instead of 16 on the digits
+    int p0[4], h0[4], p1[4], h1[4];
+    static_for<0, 4>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      p0[u] = d0[4 * u] + (d0[4 * u + 1] << 8);
+      h0[u] = d0[4 * u + 2] + (d0[4 * u + 3] << 8);
+      p1[u] = d1[4 * u] + (d1[4 * u + 1] << 8);
+      h1[u] = d1[4 * u + 2] + (d1[4 * u + 3] << 8);
+      swap32(p0[u], p1[u]);  // p0: own limb 2u, p1: own limb 2u + 1
+      swap32(h0[u], h1[u]);
     });
     static_for<0, 8>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       constexpr int q = 8 * mt + r, u = r >> 1;
       if constexpr (q < kL) {
-        const v16i& d = (r & 1) ? d1 : d0;
         // limb q = c0 + 2^8 c1 + 2^16 (c2 + 2^8 c3) + t_lo + cadd (- h) + carry;
         // the first terms of p stay in int32 (|c0 + 2^8 c1| < 1.27e9, t_lo, cadd
         // and h < 2^28), h * 2^16 + p + carry is two v_mad_i64_i32
-        int p = d[4 * u] + (d[4 * u + 1] << 8);
+        int p = (r & 1) ? p1[u] : p0[u];
         if constexpr (q < kFoldF) p += (int)t[q];
         p += (int)cadd[q];
         if constexpr (SUB_H && q < kHL) p -= (int)hl[q];
-        const int h = d[4 * u + 2] + (d[4 * u + 3] << 8);
+        const int h = (r & 1) ? h1[u] : h0[u];
         const int64_t v = mad_i64(h, 65536, mad_i64(p, 1, carry));
         x[q] = (uint32_t)v & kLimbMask;
         carry = v >> kLimbBits;
