@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MOCHI_ABI_VERSION 2
+#define MOCHI_ABI_VERSION 3
 #define MOCHI_RSA_BYTES 256     /* RSA-2048 modulus / signature size            */
 #define MOCHI_RSA_E 65537u      /* the only public exponent supported          */
 #define MOCHI_TXN_HASH_BYTES 128 /* lowercase-hex SHA-512 (Utils.java:135-153)  */
@@ -528,6 +528,35 @@ mochi_batcher* mochi_batcher_create(mochi_ctx* ctx, const mochi_params* params, 
  * are in flight.  The batcher borrows the contexts. */
 mochi_batcher* mochi_batcher_create_multi(mochi_ctx* const* ctxs, uint32_t n_ctx, const mochi_params* params,
                                           uint32_t max_msgs, uint32_t max_wait_us, int with_op_flags);
+typedef void (*mochi_verdict_cb)(void* user, int rc, const mochi_verdict1* verdict);
+
+/* One Write2ToServer request (ABI 3): the message body plus the receiving
+ * server's per-op state and optional per-op outputs.  Everything stays owned by
+ * the caller and must stay valid until the verdict is delivered. */
+typedef struct mochi_write2_request {
+  const uint8_t* msg;            /* Write2ToServer body (ProtocolMessage field 110)            */
+  uint32_t msg_len;
+  uint32_t n_ops;                /* operations in the message's transaction                   */
+  const uint8_t* op_flags;       /* [n_ops] MOCHI_OP_* (batcher created with with_op_flags)     */
+  const int64_t* op_object_ts;   /* [n_ops] stored currentC timestamp, read iff HAS_CURRENT_C;
+                                    NULL = none                                                */
+  const uint8_t* expected_hash;  /* [128] objectSHA512(transaction), lowercase hex              */
+  uint8_t* op_decision;          /* [n_ops] out: enum mochi_op_decision (NULL = not wanted)     */
+  uint32_t* op_g0;               /* [n_ops] out: certificate-relative index of g0               */
+  int64_t* op_ts;                /* [n_ops] out: g0's timestamp (what applyOperation records)   */
+} mochi_write2_request;
+
+/* Blocks until this request's verdict is in `out` (and its per-op outputs are
+ * written).  Thread-safe.  Returns the status of the batch call that carried
+ * it.  This is the call a server's Write2 handler makes in place of
+ * InMemoryDataStore.processWrite2ToServer (InMemoryDataStore.java:641-666): the
+ * per-op decision says which operations applyOperation / readOperation runs.
+ * MOCHI_EINVAL from a completion callback running on this batcher. */
+int mochi_batcher_verify_request(mochi_batcher* b, const mochi_write2_request* req, mochi_verdict1* out);
+/* Non-blocking form: cb(user, rc, &verdict) runs on a flusher thread once the
+ * batch is verified, after the per-op outputs are written.  Callbacks must not
+ * call mochi_batcher_destroy / _verify* on the batcher running them. */
+int mochi_batcher_submit_request(mochi_batcher* b, const mochi_write2_request* req, mochi_verdict_cb cb, void* user);
 /* Blocks until this message's verdict is in `out`.  Thread-safe.  Returns the
  * status of the batch call that carried it. */
 int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
@@ -538,12 +567,45 @@ int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len,
  * msg / op_flags / expected_hash must stay valid until the callback.  With
  * thousands of requests in flight the batches grow to max_msgs, so throughput
  * follows the bulk wire path instead of 1 / latency per blocked thread. */
-typedef void (*mochi_verdict_cb)(void* user, int rc, const mochi_verdict1* verdict);
 int mochi_batcher_submit(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
                          uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict_cb cb, void* user);
 int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs);
-/* Drains pending requests, then stops the flusher. */
+/* Drains pending requests, then stops the flushers.  Not from a callback of
+ * the same batcher (ignored there: the flusher would have to join itself). */
 void mochi_batcher_destroy(mochi_batcher* b);
+
+/* ------------------------------------------------------------------------
+ * Cluster configuration (ABI 3): the reference's properties file
+ * (ClusterConfiguration.loadInitialConfigurationFromProperties,
+ * ClusterConfiguration.java:138-187; config/sample_config): _CONFIG_SERVERS,
+ * _CONFIG_BFT_REPLICATION, _CONFIG_SERVER_<id>_URL, _CONFIG_SERVER_<id>_TOKENS.
+ * Host only.  Errors (MOCHI_EINVAL + mochi_last_error()) where the reference
+ * throws: a server without URL, a token >= 1024 or mapped twice, a token left
+ * unassigned, no replication factor, R < 4 or R > the token owners (:182-184).
+ * ------------------------------------------------------------------------ */
+typedef struct mochi_config mochi_config;
+mochi_config* mochi_config_load(const char* path);
+/* The same from the properties text itself. */
+mochi_config* mochi_config_parse(const char* text, uint64_t len);
+void mochi_config_free(mochi_config* c);
+/* R (_CONFIG_BFT_REPLICATION) and M = getServerMajority() = 2*(R/3)+1. */
+uint32_t mochi_config_replication(const mochi_config* c);
+uint32_t mochi_config_majority(const mochi_config* c);
+/* Servers in _CONFIG_SERVERS order: id and URL (NUL-terminated, owned by c). */
+uint32_t mochi_config_n_servers(const mochi_config* c);
+const char* mochi_config_server_id(const mochi_config* c, uint32_t i);
+const char* mochi_config_server_url(const mochi_config* c, uint32_t i);
+/* getServersForObject(key) (ClusterConfiguration.java:194-226): R indices into
+ * the server table, in replica order.  Faithful to the reference, whose loop
+ * reads token i instead of ithTokenValue (:215), so every key maps to the
+ * owners of tokens 0..R-1; key = UTF-8 bytes (hashed as Java String.hashCode). */
+int mochi_config_servers_for_key(const mochi_config* c, const uint8_t* key, uint32_t key_len, uint32_t* idx_out);
+/* Server-id table of the replica set of `key` (or of tokens 0..R-1 for key =
+ * NULL), laid out for mochi_ctx_set_server_ids: ids_out = the ids back to back,
+ * id_off[R+1].  ids_cap = capacity of ids_out; returns the bytes needed (or
+ * < 0 on error), writing nothing beyond ids_cap. */
+int64_t mochi_config_replica_ids(const mochi_config* c, const uint8_t* key, uint32_t key_len, uint8_t* ids_out,
+                                 uint64_t ids_cap, uint32_t* id_off);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU: certificates are independent, so a batch is cut
@@ -578,10 +640,14 @@ mochi_ctx* mochi_mctx_context(mochi_mctx* m, int i);
 int mochi_mctx_set_server_ids(mochi_mctx* m, const uint8_t* ids, const uint32_t* id_off, uint32_t n_ids);
 /* Host batch across the devices: each device runs mochi_verify_batch on its
  * shard (outputs land in their slices of `out`; grant_valid_bits is not
- * supported here, use grant_flags), then the shard bitmaps are all-gathered and
- * out->cert_accept_bits is assembled from device 0's copy. */
+ * supported here, use grant_flags), then each device's accept bitmap is
+ * all-gathered from where the verify left it in device memory (no host
+ * round trip) and out->cert_accept_bits is assembled from one copy of device
+ * 0's gathered buffer.  The per-device contexts must not be used by other
+ * threads during the call. */
 int mochi_mverify_batch(mochi_mctx* m, const mochi_batch* batch, const mochi_params* params, mochi_verdicts* out);
-/* Write2ToServer messages across the devices (shards by wire bytes). */
+/* Write2ToServer messages across the devices (shards by wire bytes); as
+ * mochi_verify_write2, the grant-level outputs must be NULL (MOCHI_EINVAL). */
 int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* batch, const mochi_params* params,
                          mochi_verdicts* out, uint8_t* msg_status);
 /* After a call: device i's all-gathered buffer (n_devices slots of

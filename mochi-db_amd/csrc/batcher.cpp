@@ -6,12 +6,16 @@
 // ThreadPoolExecutor of core 2 / max 20 threads (MochiServer.java:36-40).  One
 // certificate is far too little work for a GPU launch, so the drop-in keeps
 // that blocking per-request call and coalesces the requests of all threads:
-// callers enqueue their message and sleep; one flusher thread takes up to
+// callers enqueue their message and sleep; a flusher thread takes up to
 // max_msgs pending messages (or whatever is pending once the oldest has waited
 // max_wait_us), verifies them with ONE mochi_verify_write2 call, and wakes each
 // caller with its own verdict.  While a batch is on the GPU the next one
 // accumulates, so the batch size follows the offered load; with several
 // contexts (mochi_batcher_create_multi) several batches are in flight at once.
+//
+// Each flusher assembles its batch straight into pinned host memory
+// (mochi_host_alloc), which mochi_verify_write2 DMAs in place: a request's
+// bytes are copied once, from the caller's buffer into the batch.
 //
 // Built only on the public C ABI (include/mochi_hip.h).
 #include <chrono>
@@ -27,17 +31,32 @@
 namespace {
 
 struct Request {
-  const uint8_t* msg;
-  uint32_t msg_len;
-  const uint8_t* op_flags;  // may be null (every op LOCAL|HAS_SVOC)
-  uint32_t n_ops;
-  const uint8_t* expected_hash;
+  mochi_write2_request r;  // caller's buffers (valid until completion)
   std::chrono::steady_clock::time_point t_enq;
   mochi_verdict1* out;  // blocking call: the caller's verdict slot
-  mochi_verdict_cb cb;  // mochi_batcher_submit: completion callback (heap request)
+  mochi_verdict_cb cb;  // submit: completion callback (heap request)
   void* user;
   int rc = 0;
   bool done = false;
+};
+
+// A grow-only pinned host array (mochi_host_alloc), reused across batches.
+template <typename T>
+struct Pinned {
+  T* p = nullptr;
+  size_t cap = 0;
+  ~Pinned() { mochi_host_free(p); }
+  bool reserve(size_t n) {
+    if (n <= cap) return true;
+    size_t c = cap ? cap : 256;
+    while (c < n) c *= 2;
+    T* q = (T*)mochi_host_alloc(sizeof(T) * c);
+    if (!q) return false;
+    mochi_host_free(p);
+    p = q;
+    cap = c;
+    return true;
+  }
 };
 
 // One flusher per context: with n contexts, n batches are in flight at once
@@ -46,11 +65,19 @@ struct Request {
 struct Flusher {
   mochi_ctx* ctx;
   std::thread th;
-  // batch assembly buffers (this flusher's thread only)
-  std::vector<uint8_t> wire, flags, hashes, status, reason, fail_op;
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> len, flags_off, accept;
+  // batch assembly (this flusher's thread only): inputs pinned, outputs host
+  Pinned<uint8_t> wire, flags, hashes;
+  Pinned<uint64_t> off;
+  Pinned<uint32_t> len, flags_off;
+  Pinned<int64_t> ots;
+  std::vector<uint8_t> status, reason, fail_op, op_dec;
+  std::vector<uint32_t> accept, op_g0;
+  std::vector<int64_t> op_ts;
 };
+
+// the batcher whose flusher runs on this thread (a callback re-entering the
+// batcher it runs on would deadlock a single-context batcher)
+thread_local const void* t_flushing = nullptr;
 
 }  // namespace
 
@@ -65,20 +92,32 @@ struct mochi_batcher {
   uint64_t n_batches = 0, n_msgs = 0;
   std::vector<Flusher> fl;
 
-  void run(Flusher& f) {
-    std::vector<Request*> batch, owned;
+  // Takes the next batch: waits for work, then for a full batch or for the
+  // oldest pending request's deadline (re-evaluated whenever a sibling flusher
+  // took the queue's head).  Returns false when stopped and drained.
+  bool take(std::vector<Request*>& batch) {
+    std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv_work.wait(lk, [&] { return stop || !q.empty(); });
-        if (q.empty() && stop) return;
-        // wait for a full batch or for the oldest request's deadline
+      cv_work.wait(lk, [&] { return stop || !q.empty(); });
+      if (q.empty()) return false;  // stopped and drained
+      while (!stop && !q.empty() && q.size() < max_msgs) {
         const auto deadline = q.front()->t_enq + std::chrono::microseconds(max_wait_us);
-        cv_work.wait_until(lk, deadline, [&] { return stop || q.size() >= max_msgs; });
-        const size_t n = q.size() < max_msgs ? q.size() : max_msgs;
-        batch.assign(q.begin(), q.begin() + n);
-        q.erase(q.begin(), q.begin() + n);
+        if (std::chrono::steady_clock::now() >= deadline) break;
+        cv_work.wait_until(lk, deadline);
       }
+      if (q.empty()) continue;  // a sibling flusher took it: never verify M = 0
+      const size_t n = q.size() < max_msgs ? q.size() : max_msgs;
+      batch.assign(q.begin(), q.begin() + n);
+      q.erase(q.begin(), q.begin() + n);
+      if (!q.empty()) cv_work.notify_one();  // leave the rest to an idle sibling now
+      return true;
+    }
+  }
+
+  void run(Flusher& f) {
+    t_flushing = this;
+    std::vector<Request*> batch, owned;
+    while (take(batch)) {
       verify(f, batch);  // fills the blocking callers' slots, runs the submitters' callbacks
       // the submitted (heap) requests are freed here; a blocking caller's request
       // lives on its stack and may be gone the moment it sees `done`, so it is
@@ -99,77 +138,109 @@ struct mochi_batcher {
   }
 
   void verify(Flusher& f, const std::vector<Request*>& batch) {
-    auto& wire = f.wire;
-    auto& flags = f.flags;
-    auto& hashes = f.hashes;
-    auto& status = f.status;
-    auto& reason = f.reason;
-    auto& fail_op = f.fail_op;
-    auto& off = f.off;
-    auto& len = f.len;
-    auto& flags_off = f.flags_off;
-    auto& accept = f.accept;
     const uint32_t M = (uint32_t)batch.size();
     size_t total = 0, n_ops = 0;
-    const bool any_flags = with_op_flags;
-    for (Request* r : batch) {
-      total += r->msg_len;
-      n_ops += r->n_ops;
+    bool any_ts = false, any_op_out = false;
+    for (Request* q : batch) {
+      total += q->r.msg_len;
+      n_ops += q->r.n_ops;
+      any_ts |= q->r.op_object_ts != nullptr;
+      any_op_out |= q->r.op_decision || q->r.op_g0 || q->r.op_ts;
     }
-    wire.resize(total ? total : 1);
-    off.resize(M);
-    len.resize(M);
-    hashes.resize((size_t)M * MOCHI_TXN_HASH_BYTES);
-    flags_off.resize(M + 1);
-    flags.resize(n_ops ? n_ops : 1);
-    size_t pos = 0, op = 0;
-    for (uint32_t i = 0; i < M; i++) {
-      Request* r = batch[i];
-      memcpy(wire.data() + pos, r->msg, r->msg_len);
-      off[i] = pos;
-      len[i] = r->msg_len;
-      pos += r->msg_len;
-      memcpy(hashes.data() + (size_t)i * MOCHI_TXN_HASH_BYTES, r->expected_hash, MOCHI_TXN_HASH_BYTES);
-      flags_off[i] = (uint32_t)op;
-      for (uint32_t j = 0; j < r->n_ops; j++)
-        flags[op + j] = r->op_flags ? r->op_flags[j] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
-      op += r->n_ops;
+    const bool flags_in = with_op_flags;
+    int rc = MOCHI_OK;
+    if (!f.wire.reserve(total ? total : 1) || !f.off.reserve(M) || !f.len.reserve(M) ||
+        !f.hashes.reserve((size_t)M * MOCHI_TXN_HASH_BYTES) || !f.flags_off.reserve(M + 1) ||
+        !f.flags.reserve(n_ops ? n_ops : 1) || (any_ts && !f.ots.reserve(n_ops ? n_ops : 1)))
+      rc = MOCHI_ENOMEM;
+    if (rc == MOCHI_OK) {
+      size_t pos = 0, op = 0;
+      for (uint32_t i = 0; i < M; i++) {
+        const mochi_write2_request& r = batch[i]->r;
+        memcpy(f.wire.p + pos, r.msg, r.msg_len);
+        f.off.p[i] = pos;
+        f.len.p[i] = r.msg_len;
+        pos += r.msg_len;
+        memcpy(f.hashes.p + (size_t)i * MOCHI_TXN_HASH_BYTES, r.expected_hash, MOCHI_TXN_HASH_BYTES);
+        f.flags_off.p[i] = (uint32_t)op;
+        for (uint32_t j = 0; j < r.n_ops; j++) {
+          f.flags.p[op + j] = r.op_flags ? r.op_flags[j] : (uint8_t)(MOCHI_OP_LOCAL | MOCHI_OP_HAS_SVOC);
+          if (any_ts) f.ots.p[op + j] = r.op_object_ts ? r.op_object_ts[j] : 0;
+        }
+        op += r.n_ops;
+      }
+      f.flags_off.p[M] = (uint32_t)op;
+      mochi_write2_batch w;
+      memset(&w, 0, sizeof w);
+      w.n_msgs = M;
+      w.wire_len = total;
+      w.wire = f.wire.p;
+      w.msg_off = f.off.p;
+      w.msg_len = f.len.p;
+      // without per-op flags the decoder's default (LOCAL|HAS_SVOC) applies
+      w.op_flags_off = flags_in ? f.flags_off.p : nullptr;
+      w.op_flags = flags_in ? f.flags.p : nullptr;
+      w.op_object_ts = flags_in && any_ts ? f.ots.p : nullptr;
+      w.expected_hash = f.hashes.p;
+      f.accept.assign((M + 31) / 32, 0);
+      f.reason.resize(M);
+      f.fail_op.resize(M);
+      f.status.resize(M);
+      const bool op_out = flags_in && any_op_out;
+      if (op_out) {
+        f.op_dec.resize(n_ops ? n_ops : 1);
+        f.op_g0.resize(n_ops ? n_ops : 1);
+        f.op_ts.resize(n_ops ? n_ops : 1);
+      }
+      mochi_verdicts v;
+      memset(&v, 0, sizeof v);
+      v.cert_accept_bits = f.accept.data();
+      v.cert_reason = f.reason.data();
+      v.cert_fail_op = f.fail_op.data();
+      v.op_decision = op_out ? f.op_dec.data() : nullptr;
+      v.op_g0 = op_out ? f.op_g0.data() : nullptr;
+      v.op_ts = op_out ? f.op_ts.data() : nullptr;
+      rc = mochi_verify_write2(f.ctx, &w, &params, &v, f.status.data());
+      if (rc == MOCHI_OK && op_out)
+        for (uint32_t i = 0; i < M; i++) {
+          const mochi_write2_request& r = batch[i]->r;
+          const size_t o0 = f.flags_off.p[i];
+          for (uint32_t j = 0; j < r.n_ops; j++) {
+            if (r.op_decision) r.op_decision[j] = f.op_dec[o0 + j];
+            if (r.op_g0) r.op_g0[j] = f.op_g0[o0 + j];
+            if (r.op_ts) r.op_ts[j] = f.op_ts[o0 + j];
+          }
+        }
     }
-    flags_off[M] = (uint32_t)op;
-    mochi_write2_batch w;
-    memset(&w, 0, sizeof w);
-    w.n_msgs = M;
-    w.wire_len = total;
-    w.wire = wire.data();
-    w.msg_off = off.data();
-    w.msg_len = len.data();
-    // without per-op flags the decoder's default (LOCAL|HAS_SVOC) applies
-    w.op_flags_off = any_flags ? flags_off.data() : nullptr;
-    w.op_flags = any_flags ? flags.data() : nullptr;
-    w.expected_hash = hashes.data();
-    accept.assign((M + 31) / 32, 0);
-    reason.resize(M);
-    fail_op.resize(M);
-    status.resize(M);
-    mochi_verdicts v;
-    memset(&v, 0, sizeof v);
-    v.cert_accept_bits = accept.data();
-    v.cert_reason = reason.data();
-    v.cert_fail_op = fail_op.data();
-    const int rc = mochi_verify_write2(f.ctx, &w, &params, &v, status.data());
     for (uint32_t i = 0; i < M; i++) {
       Request* r = batch[i];
       r->rc = rc;
       mochi_verdict1 v{};
       if (rc == MOCHI_OK) {
-        v.accepted = (uint8_t)((accept[i >> 5] >> (i & 31)) & 1u);
-        v.reason = reason[i];
-        v.fail_op = fail_op[i];
-        v.msg_status = status[i];
+        v.accepted = (uint8_t)((f.accept[i >> 5] >> (i & 31)) & 1u);
+        v.reason = f.reason[i];
+        v.fail_op = f.fail_op[i];
+        v.msg_status = f.status[i];
       }
       if (r->cb) r->cb(r->user, rc, &v);
       else if (rc == MOCHI_OK) *r->out = v;
     }
+  }
+
+  int check(const mochi_write2_request* r) const {
+    if (!r || (!r->msg && r->msg_len) || !r->expected_hash) return MOCHI_EINVAL;
+    if (with_op_flags ? (r->op_flags == nullptr && r->n_ops != 0)
+                      : (r->op_flags != nullptr || r->n_ops != 0 || r->op_object_ts || r->op_decision || r->op_g0 ||
+                         r->op_ts))
+      return MOCHI_EINVAL;
+    if (t_flushing == this) return MOCHI_EINVAL;  // from a callback this batcher is running
+    return MOCHI_OK;
+  }
+
+  void enqueue(Request* r) {  // mu held
+    q.push_back(r);
+    if (q.size() == 1) cv_work.notify_one();
+    else if (q.size() >= max_msgs) cv_work.notify_all();  // whichever flusher is idle takes it
   }
 };
 
@@ -199,40 +270,29 @@ mochi_batcher* mochi_batcher_create(mochi_ctx* ctx, const mochi_params* params, 
   return mochi_batcher_create_multi(&ctx, 1, params, max_msgs, max_wait_us, with_op_flags);
 }
 
-int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
-                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict1* out) {
-  if (!b || (!msg && msg_len) || !expected_hash || !out) return MOCHI_EINVAL;
-  if (b->with_op_flags ? (op_flags == nullptr && n_ops != 0) : (op_flags != nullptr || n_ops != 0))
-    return MOCHI_EINVAL;
+int mochi_batcher_verify_request(mochi_batcher* b, const mochi_write2_request* req, mochi_verdict1* out) {
+  if (!b || !out) return MOCHI_EINVAL;
+  int rc = b->check(req);
+  if (rc) return rc;
   Request r;
-  r.msg = msg;
-  r.msg_len = msg_len;
-  r.op_flags = op_flags;
-  r.n_ops = n_ops;
-  r.expected_hash = expected_hash;
+  r.r = *req;
   r.out = out;
   r.cb = nullptr;
   r.user = nullptr;
   r.t_enq = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lk(b->mu);
   if (b->stop) return MOCHI_EINVAL;
-  b->q.push_back(&r);
-  if (b->q.size() == 1 || b->q.size() >= b->max_msgs) b->cv_work.notify_one();
+  b->enqueue(&r);
   b->cv_done.wait(lk, [&] { return r.done; });
   return r.rc;
 }
 
-int mochi_batcher_submit(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
-                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict_cb cb, void* user) {
-  if (!b || (!msg && msg_len) || !expected_hash || !cb) return MOCHI_EINVAL;
-  if (b->with_op_flags ? (op_flags == nullptr && n_ops != 0) : (op_flags != nullptr || n_ops != 0))
-    return MOCHI_EINVAL;
+int mochi_batcher_submit_request(mochi_batcher* b, const mochi_write2_request* req, mochi_verdict_cb cb, void* user) {
+  if (!b || !cb) return MOCHI_EINVAL;
+  int rc = b->check(req);
+  if (rc) return rc;
   Request* r = new Request();
-  r->msg = msg;
-  r->msg_len = msg_len;
-  r->op_flags = op_flags;
-  r->n_ops = n_ops;
-  r->expected_hash = expected_hash;
+  r->r = *req;
   r->out = nullptr;
   r->cb = cb;
   r->user = user;
@@ -242,9 +302,32 @@ int mochi_batcher_submit(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len,
     delete r;
     return MOCHI_EINVAL;
   }
-  b->q.push_back(r);
-  if (b->q.size() == 1 || b->q.size() >= b->max_msgs) b->cv_work.notify_one();
+  b->enqueue(r);
   return MOCHI_OK;
+}
+
+int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
+                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict1* out) {
+  mochi_write2_request r;
+  memset(&r, 0, sizeof r);
+  r.msg = msg;
+  r.msg_len = msg_len;
+  r.op_flags = op_flags;
+  r.n_ops = n_ops;
+  r.expected_hash = expected_hash;
+  return mochi_batcher_verify_request(b, &r, out);
+}
+
+int mochi_batcher_submit(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
+                         uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict_cb cb, void* user) {
+  mochi_write2_request r;
+  memset(&r, 0, sizeof r);
+  r.msg = msg;
+  r.msg_len = msg_len;
+  r.op_flags = op_flags;
+  r.n_ops = n_ops;
+  r.expected_hash = expected_hash;
+  return mochi_batcher_submit_request(b, &r, cb, user);
 }
 
 int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs) {
@@ -256,7 +339,7 @@ int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs) {
 }
 
 void mochi_batcher_destroy(mochi_batcher* b) {
-  if (!b) return;
+  if (!b || t_flushing == b) return;  // never from one of its own callbacks (it would join itself)
   {
     std::lock_guard<std::mutex> lk(b->mu);
     b->stop = true;

@@ -227,6 +227,8 @@ int make_fold_key(const uint8_t* n_be, mochi::FoldKey* f) {
 }  // namespace
 
 namespace mochi {
+// multi.cpp: the device accept bitmap of the context's last host-path call
+const uint32_t* ctx_last_accept_dev(mochi_ctx* c, uint32_t* words, int* device, hipStream_t* stream);
 int set_error(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -268,10 +270,25 @@ struct mochi_ctx {
       w2_mgo, w2_ots, w2_okoff, w2_oklen;
   PinnedBuf w2_tot;
   hipEvent_t ev_tot = nullptr;
+  // the last host-path call's certificate accept bitmap on the device (a slice
+  // of dev_out, valid until the next call on this context; nullptr when the
+  // device copy is not the final verdict, e.g. after host fallback decisions):
+  // multi.cpp all-gathers it in place of re-uploading the host bits
+  const uint32_t* acc_dev = nullptr;
+  uint32_t acc_words = 0;
   // per-stage profiling (mochi_ctx_set_profiling): one event set per verify call
   bool profiling = false;
   std::vector<std::vector<hipEvent_t>> prof_sets;
 };
+
+namespace mochi {
+const uint32_t* ctx_last_accept_dev(mochi_ctx* c, uint32_t* words, int* device, hipStream_t* stream) {
+  *words = c->acc_words;
+  *device = c->device;
+  *stream = c->stream;
+  return c->acc_dev;
+}
+}  // namespace mochi
 
 extern "C" {
 
@@ -589,6 +606,8 @@ enum Seg {
 
 int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o) {
   const uint32_t N = b->n_grants, C = b->n_certs, O = b->n_ops;
+  c->acc_dev = nullptr;
+  c->acc_words = 0;
   const bool mg = b->cert_mg_off != nullptr;
   // --- plan chunks ---
   struct Chunk {
@@ -801,6 +820,8 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
                          (size_t)O, sizeof(uint32_t) * O, sizeof(int64_t) * O};
   for (int i = 0; i < 9; i++)
     if (dsts[i] && lens[i]) memcpy(dsts[i], pout + offs[i], lens[i]);
+  c->acc_dev = (const uint32_t*)(dout + o_acc);
+  c->acc_words = (uint32_t)(nbits_c / 4);
   return MOCHI_OK;
 }
 
@@ -1250,6 +1271,8 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   }
   if (c->n_ids != c->n_keys) return fail(MOCHI_EINVAL, "server ids not set (mochi_ctx_set_server_ids)");
   std::lock_guard<std::mutex> lk(c->mu);
+  c->acc_dev = nullptr;
+  c->acc_words = 0;
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
@@ -1354,6 +1377,10 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   uint8_t* pout = (uint8_t*)c->pin_out.p;
   uint32_t* tot = (uint32_t*)c->w2_tot.p;
   hipStream_t st = c->stream;
+  // sources already in pinned memory (mochi_host_alloc) are DMA'd in place;
+  // the rebased op_flags_off CSR (segment 3) is always staged
+  bool pinned[7];
+  for (int i = 0; i < 7; i++) pinned[i] = i != 3 && is_pinned(seg_src(ch[0], i));
   std::vector<mochi_write2_batch> dws(nch);
   std::vector<mochi::W2Args> args(nch);
   HIP_TRY(scratch_acquire(c, st));
@@ -1402,8 +1429,10 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     for (int i = 0; i < 7; i++) {
       const size_t n = seg_bytes(k, i);
       if (!n) continue;
-      if (i != 3) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
-      HIP_TRY(hipMemcpyAsync(din + k.seg[i], pin + k.seg[i], n, hipMemcpyHostToDevice, c->s_in));
+      const void* src = pin + k.seg[i];
+      if (pinned[i]) src = seg_src(k, i);  // DMA'd in place (e.g. the batcher's pinned batch)
+      else if (i != 3) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
+      HIP_TRY(hipMemcpyAsync(din + k.seg[i], src, n, hipMemcpyHostToDevice, c->s_in));
     }
     HIP_TRY(hipEventRecord(c->chunk_ev[2 * j], c->s_in));
     mochi_write2_batch& dw = dws[j];
@@ -1480,8 +1509,13 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   if (o->op_decision) memcpy(o->op_decision, pout + o_dec, O_in);
   if (o->op_g0) memcpy(o->op_g0, pout + o_g0, 4 * O_in);
   if (o->op_ts) memcpy(o->op_ts, pout + o_ots, 8 * O_in);
-  if (!fallback.empty()) return decide_fallback(c, w, p, o, fallback);
-  return MOCHI_OK;
+  c->acc_dev = (const uint32_t*)(dout + o_acc);
+  c->acc_words = (uint32_t)(nbits / 4);
+  if (fallback.empty()) return MOCHI_OK;
+  rc = decide_fallback(c, w, p, o, fallback);
+  c->acc_dev = nullptr;  // the host decided some verdicts (and the fallback batch reused dev_out)
+  c->acc_words = 0;
+  return rc;
 }
 
 int mochi_fold_matrix(const uint8_t* modulus_be, int8_t* img, uint32_t* cadd) {

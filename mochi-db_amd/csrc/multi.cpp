@@ -28,6 +28,8 @@
 
 namespace mochi {
 int set_error(int code, const std::string& msg);  // capi.cpp: the text mochi_last_error() returns
+// capi.cpp: the accept bitmap of the context's last host-path call, on its device
+const uint32_t* ctx_last_accept_dev(mochi_ctx* c, uint32_t* words, int* device, hipStream_t* stream);
 }
 
 namespace {
@@ -295,9 +297,14 @@ void slice_batch(const mochi_batch* B, uint32_t c0, uint32_t c1, SubBatch& s) {
   }
 }
 
-// The all-gather step: each device's shard bits (host) go into its slot of the
-// device's gather buffer, one ncclAllGather per device (one thread each), and
-// device 0's full buffer is assembled into `bits_out`.
+// The all-gather step.  Each device's shard verdicts are already on that
+// device: the accept bitmap of the context call that just returned (a slice of
+// its output buffer).  Per device (one thread each) it is copied device to
+// device into the device's slot of its gather buffer (zero-padded to W words),
+// then one ncclAllGather fills every device's buffer, and bits_out comes from
+// ONE device-to-host copy of device 0's.  A context whose device bitmap is not
+// the final verdict (messages decided by the host fallback decoder) uploads its
+// host bits into its slot instead.
 int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::vector<std::vector<uint32_t>>& shard_bits,
                 uint32_t* bits_out) {
   const int n = (int)m->devices.size();
@@ -320,10 +327,21 @@ int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::
       m->gathered_cap[i] = bytes;
     }
     uint32_t* slot = m->gathered[i] + (size_t)W * i;
-    std::vector<uint32_t> padded(W, 0u);
-    memcpy(padded.data(), shard_bits[i].data(), 4 * shard_bits[i].size());
-    if (hipMemcpyAsync(slot, padded.data(), 4 * (size_t)W, hipMemcpyHostToDevice, m->stream[i]) != hipSuccess ||
-        ncclAllGather(slot, m->gathered[i], W, ncclUint32, m->comm[i], m->stream[i]) != ncclSuccess ||
+    const uint32_t need = words(cert_lo[i + 1] - cert_lo[i]);  // <= W
+    uint32_t dev_words = 0;
+    int dev = -1;
+    hipStream_t cst = nullptr;
+    const uint32_t* d = mochi::ctx_last_accept_dev(m->ctx[i], &dev_words, &dev, &cst);
+    hipError_t e = hipMemsetAsync(slot, 0, 4 * (size_t)W, m->stream[i]);
+    if (e == hipSuccess && need) {
+      if (d && dev == m->devices[i] && dev_words >= need)
+        e = hipMemcpyAsync(slot, d, 4 * (size_t)need, hipMemcpyDeviceToDevice, m->stream[i]);
+      else {
+        const size_t have = shard_bits[i].size() < need ? shard_bits[i].size() : need;
+        e = hipMemcpyAsync(slot, shard_bits[i].data(), 4 * have, hipMemcpyHostToDevice, m->stream[i]);
+      }
+    }
+    if (e != hipSuccess || ncclAllGather(slot, m->gathered[i], W, ncclUint32, m->comm[i], m->stream[i]) != ncclSuccess ||
         hipStreamSynchronize(m->stream[i]) != hipSuccess)
       rc[i] = MOCHI_EHIP;
   };
@@ -360,7 +378,7 @@ int mochi_mverify_batch(mochi_mctx* m, const mochi_batch* b, const mochi_params*
     SubBatch s;
     slice_batch(b, lo[i], lo[i + 1], s);
     const uint32_t g0 = b->cert_grant_off[lo[i]], o0 = b->cert_op_off[lo[i]];
-    bits[i].assign(words(lo[i + 1] - lo[i]) + 1, 0u);
+    bits[i].assign(words(lo[i + 1] - lo[i]) + 1, 0u);  // +1: a non-empty vector for empty shards
     mochi_verdicts v;
     memset(&v, 0, sizeof v);
     v.grant_flags = o->grant_flags ? o->grant_flags + g0 : nullptr;
@@ -385,6 +403,8 @@ int mochi_mverify_batch(mochi_mctx* m, const mochi_batch* b, const mochi_params*
 int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
                          uint8_t* msg_status) {
   if (!m || !w || !p || !o || (!o->cert_accept_bits && w->n_msgs)) return mfail(MOCHI_EINVAL, "null argument");
+  if (o->grant_flags || o->grant_ts || o->grant_valid_bits)  // as mochi_verify_write2 (check_write2_header)
+    return mfail(MOCHI_EINVAL, "grant-level outputs are not produced on the wire path (must be NULL)");
   const int n = (int)m->devices.size();
   // shard by wire bytes (a proxy for grants: the messages are not decoded yet)
   std::vector<uint32_t> prefix(w->n_msgs + 1, 0);
@@ -414,7 +434,7 @@ int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* w, const mochi
       s.op_flags = w->op_flags + o0;
       if (w->op_object_ts) s.op_object_ts = w->op_object_ts + o0;
     }
-    bits[i].assign(words(m1 - m0) + 1, 0u);
+    bits[i].assign(words(m1 - m0) + 1, 0u);  // +1: a non-empty vector for empty shards
     mochi_verdicts v;
     memset(&v, 0, sizeof v);
     v.cert_accept_bits = bits[i].data();

@@ -131,7 +131,7 @@ class Verdicts_C(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -218,6 +218,27 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_host_alloc.restype = vp
     lib.mochi_host_alloc.argtypes = [ctypes.c_uint64]
     lib.mochi_host_free.argtypes = [vp]
+    # ABI 3: per-request batcher calls with stored state + per-op outputs; cluster config
+    lib.mochi_batcher_verify_request.argtypes = [vp, ctypes.POINTER(Write2Request_C), ctypes.POINTER(Verdict1_C)]
+    lib.mochi_batcher_submit_request.argtypes = [vp, ctypes.POINTER(Write2Request_C), VERDICT_CB, vp]
+    lib.mochi_config_load.restype = vp
+    lib.mochi_config_load.argtypes = [ctypes.c_char_p]
+    lib.mochi_config_parse.restype = vp
+    lib.mochi_config_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    lib.mochi_config_free.argtypes = [vp]
+    lib.mochi_config_replication.restype = u32
+    lib.mochi_config_replication.argtypes = [vp]
+    lib.mochi_config_majority.restype = u32
+    lib.mochi_config_majority.argtypes = [vp]
+    lib.mochi_config_n_servers.restype = u32
+    lib.mochi_config_n_servers.argtypes = [vp]
+    lib.mochi_config_server_id.restype = ctypes.c_char_p
+    lib.mochi_config_server_id.argtypes = [vp, u32]
+    lib.mochi_config_server_url.restype = ctypes.c_char_p
+    lib.mochi_config_server_url.argtypes = [vp, u32]
+    lib.mochi_config_servers_for_key.argtypes = [vp, vp, u32, vp]
+    lib.mochi_config_replica_ids.restype = ctypes.c_int64
+    lib.mochi_config_replica_ids.argtypes = [vp, vp, u32, vp, ctypes.c_uint64, vp]
     if lib.mochi_abi_version() != ABI_VERSION:
         raise MochiError("libmochi_hip ABI mismatch")
     _lib = lib
@@ -934,6 +955,44 @@ class Verdict1_C(ctypes.Structure):
 VERDICT_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Verdict1_C))
 
 
+class Write2Request_C(ctypes.Structure):
+    """mochi_write2_request (ABI 3)."""
+    _fields_ = [("msg", ctypes.c_void_p), ("msg_len", ctypes.c_uint32), ("n_ops", ctypes.c_uint32),
+                ("op_flags", ctypes.c_void_p), ("op_object_ts", ctypes.c_void_p), ("expected_hash", ctypes.c_void_p),
+                ("op_decision", ctypes.c_void_p), ("op_g0", ctypes.c_void_p), ("op_ts", ctypes.c_void_p)]
+
+
+class Write2Request:
+    """One Write2ToServer as a server receives it, with its per-op state
+    (MOCHI_OP_* flags, stored-certificate timestamps) and per-op outputs
+    (decision, g0, g0's timestamp) — the buffers live as long as this object."""
+
+    def __init__(self, msg: bytes, expected_hash: bytes, op_flags: Optional[Sequence[int]] = None,
+                 op_object_ts: Optional[Sequence[int]] = None, want_ops: bool = True):
+        self.msg = np.frombuffer(bytes(msg) or b"\x00", np.uint8).copy()
+        self.msg_len = len(msg)
+        self.expected_hash = np.frombuffer(bytes(expected_hash), np.uint8).copy()
+        assert self.expected_hash.shape[0] == TXN_HASH_BYTES
+        n = 0 if op_flags is None else len(op_flags)
+        self.op_flags = None if op_flags is None else np.asarray(op_flags, np.uint8).copy()
+        self.op_object_ts = None if op_object_ts is None else np.asarray(op_object_ts, np.int64).copy()
+        if self.op_object_ts is not None:
+            assert self.op_object_ts.shape[0] == n
+        self.op_decision = np.zeros(max(n, 1), np.uint8) if want_ops and n else None
+        self.op_g0 = np.zeros(max(n, 1), np.uint32) if want_ops and n else None
+        self.op_ts = np.zeros(max(n, 1), np.int64) if want_ops and n else None
+        self.c = Write2Request_C(_ptr(self.msg), self.msg_len, n, _ptr(self.op_flags), _ptr(self.op_object_ts),
+                                 _ptr(self.expected_hash), _ptr(self.op_decision), _ptr(self.op_g0), _ptr(self.op_ts))
+        self.result = None  # (rc, accepted, reason, fail_op, msg_status) once delivered
+
+    def ops(self):
+        """[(decision, g0, ts)] per op (after the verdict)."""
+        if self.op_decision is None:
+            return []
+        n = self.c.n_ops
+        return [(int(self.op_decision[i]), int(self.op_g0[i]), int(self.op_ts[i])) for i in range(n)]
+
+
 class Batcher:
     """mochi_batcher: blocking per-request verify, coalesced across calling threads.
     (ctypes drops the GIL during the call, so Python threads block concurrently.)"""
@@ -984,6 +1043,30 @@ class Batcher:
         if rc != OK:
             raise MochiError(f"mochi_batcher_verify rc={rc}: {_err(self.lib)}")
         return bool(out.accepted), out.reason, out.fail_op, out.msg_status
+
+    def verify_request(self, req: "Write2Request"):
+        """mochi_batcher_verify_request: blocks; fills req's per-op outputs."""
+        out = Verdict1_C()
+        rc = self.lib.mochi_batcher_verify_request(self.h, ctypes.byref(req.c), ctypes.byref(out))
+        if rc != OK:
+            raise MochiError(f"mochi_batcher_verify_request rc={rc}: {_err(self.lib)}")
+        req.result = (rc, bool(out.accepted), out.reason, out.fail_op, out.msg_status)
+        return req.result[1:]
+
+    def submit_request(self, req: "Write2Request", done):
+        """mochi_batcher_submit_request: done(req) runs on a flusher thread once
+        req.result and its per-op outputs are set."""
+        key = next(self._seq)
+
+        def fin(rc, accepted, reason, fail_op, msg_status):
+            req.result = (rc, accepted, reason, fail_op, msg_status)
+            done(req)
+
+        self._pending[key] = (req, None, None, fin)
+        rc = self.lib.mochi_batcher_submit_request(self.h, ctypes.byref(req.c), self._cb, key)
+        if rc != OK:
+            self._pending.pop(key, None)
+            raise MochiError(f"mochi_batcher_submit_request rc={rc}")
 
     def stats(self):
         b, m = ctypes.c_uint64(), ctypes.c_uint64()
@@ -1163,3 +1246,68 @@ class Comm:
         if self.h:
             self.lib.mochi_comm_destroy(self.h)
             self.h = None
+
+
+class ClusterConfig:
+    """The reference's cluster properties file (mochi_config_*;
+    ClusterConfiguration.loadInitialConfigurationFromProperties,
+    ClusterConfiguration.java:138-187)."""
+
+    def __init__(self, path: Optional[str] = None, text: Optional[str] = None):
+        self.lib = load_library()
+        if path is not None:
+            self.h = self.lib.mochi_config_load(path.encode())
+        else:
+            raw = (text or "").encode()
+            self.h = self.lib.mochi_config_parse(raw, len(raw))
+        if not self.h:
+            raise MochiError(f"mochi_config: {_err(self.lib)}")
+
+    @property
+    def replication_factor(self) -> int:
+        return int(self.lib.mochi_config_replication(self.h))
+
+    @property
+    def majority(self) -> int:
+        return int(self.lib.mochi_config_majority(self.h))
+
+    def servers(self):
+        n = self.lib.mochi_config_n_servers(self.h)
+        return [(self.lib.mochi_config_server_id(self.h, i).decode(), self.lib.mochi_config_server_url(self.h, i).decode())
+                for i in range(n)]
+
+    def servers_for_key(self, key: str):
+        """getServersForObject(key): indices into servers(), replica order."""
+        kb = key.encode()
+        out = np.zeros(self.replication_factor, np.uint32)
+        rc = self.lib.mochi_config_servers_for_key(self.h, kb, len(kb), _ptr(out))
+        if rc != OK:
+            raise MochiError(f"mochi_config_servers_for_key: {_err(self.lib)}")
+        return [int(i) for i in out]
+
+    def replica_ids(self, key: Optional[str] = None):
+        """(ids blob, id_off[R+1]) for mochi_ctx_set_server_ids."""
+        kb = key.encode() if key is not None else None
+        off = np.zeros(self.replication_factor + 1, np.uint32)
+        need = self.lib.mochi_config_replica_ids(self.h, kb, len(kb) if kb else 0, None, 0, _ptr(off))
+        if need < 0:
+            raise MochiError(f"mochi_config_replica_ids: {_err(self.lib)}")
+        blob = np.zeros(max(int(need), 1), np.uint8)
+        self.lib.mochi_config_replica_ids(self.h, kb, len(kb) if kb else 0, _ptr(blob), int(need), _ptr(off))
+        return blob[:int(need)], off
+
+    def replica_id_list(self, key: Optional[str] = None):
+        blob, off = self.replica_ids(key)
+        b = blob.tobytes()
+        return [b[off[i]:off[i + 1]].decode() for i in range(len(off) - 1)]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mochi_config_free(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -26,17 +26,26 @@ from mochi_hip import (OP_HAS_SVOC, OP_LOCAL, RSA_BYTES, TXN_HASH_BYTES, Batch, 
 
 SEED = 0x4D4F434849  # "MOCHI"
 
-# Replica IDs of config/sample_config:1 in token order 0..3 (every key maps to
-# tokens 0..R-1 because of ClusterConfiguration.java:215), plus synthetic ones.
-SERVER_IDS = [
-    "server-ed25bc93-1047-4242-b87b-2246355b020b",
-    "server-55a78d3f-783d-43ae-95c1-6d0f5f02fe0c",
-    "server-6c023c90-87ed-40d9-8f38-48cb03fa2135",
-    "server-6a3b63b2-9fc8-4f3d-97c1-0f61cb244a0c",
-    "server-synthetic-r7-0004",
-    "server-synthetic-r7-0005",
-    "server-synthetic-r7-0006",
-]
+# The cluster the synthetic certificates come from: the reference's own
+# config/sample_config (copied to tests/golden/sample_config), read by the
+# library's loader (mochi_config_load, ClusterConfiguration.java:138-187):
+# R = 4 and the replica set every key maps to (tokens 0..R-1, because of
+# ClusterConfiguration.java:215), plus three synthetic ids for R = 7.
+SAMPLE_CONFIG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                             "sample_config")
+
+
+def _sample_replicas() -> List[str]:
+    from mochi_hip import ClusterConfig
+
+    cfg = ClusterConfig(SAMPLE_CONFIG)
+    try:
+        return cfg.replica_id_list()
+    finally:
+        cfg.close()
+
+
+SERVER_IDS = _sample_replicas() + ["server-synthetic-r7-0004", "server-synthetic-r7-0005", "server-synthetic-r7-0006"]
 
 DEFAULT_KEY_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "keys")
 

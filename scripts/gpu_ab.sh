@@ -10,6 +10,6 @@ for i in 1 2; do
     v=${LIBS[$k]}; tag=$(basename $v .so)
     if [ $v = A ]; then L=""; else L="$PWD/$v"; fi
     MOCHI_HIP_LIB=$L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --headline-only ${BENCH_ARGS:-} > $OUT/ab_$tag$i.json 2> $OUT/ab_$tag$i.err || { tail -20 $OUT/ab_$tag$i.err; exit 1; }
-    python -c "import json;d=json.load(open('$OUT/ab_$tag$i.json'));print('$tag$i', round(d['value']/1e6,2),'M grants/s', d['stage_ms'])"
+    python -c "import json;d=json.load(open('$OUT/ab_$tag$i.json'));print('$tag$i', round(d['value']/1e6,2),'M grants/s', d['stage_ms'], 'ok=',d.get('correct_vs_ground_truth'))"
   done
 done

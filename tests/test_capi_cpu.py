@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert mh.load_library().mochi_abi_version() == mh.ABI_VERSION == 2
+    assert mh.load_library().mochi_abi_version() == mh.ABI_VERSION == 3
 
 
 def test_ctx_create_rejects_bad_keys():
