@@ -81,6 +81,8 @@ def parse_args():
     ap.add_argument("--headline-only", action="store_true",
                     help="only the timed device-resident steps (no side legs): the profiled run")
     ap.add_argument("--cache-dir", default=os.environ.get("MOCHI_CACHE", "/tmp/mochi_bench_cache"))
+    ap.add_argument("--no-native", action="store_true", help="skip the native batcher load driver leg")
+    ap.add_argument("--no-cluster", action="store_true", help="skip the in-process cluster (C1 / C5 proxy) leg")
     return ap.parse_args()
 
 
@@ -162,6 +164,12 @@ def main():
     cpu_certs = min(C, 250_000)  # the baseline's sample: the stream's first certificates (~1M grants at R = 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_child = start_cpu_baseline(args, R, k, cpu_flags, batch_file)
+    # native batcher load driver (microbench/batcher_load): also started before this
+    # process touches the GPU; it waits for the Write2 input file the wire leg writes
+    args.native_child = args.native_input = None
+    if rank == 0 and world == 1 and not (args.headline_only or args.no_wire or args.no_native):
+        args.native_input = os.path.join(args.cache_dir, f"w2_native_{os.getpid()}.bin")
+        args.native_child = start_batcher_native(args, args.native_input)
     torch.cuda.set_device(local_rank)
     dist = None
     comm = None
@@ -260,6 +268,7 @@ def main():
         wire = wire_path(ver, wire_s, R, strict, local_rank, stream, args) if wire_s is not None else None
         signing = sign_path(W.load_keys(1)[0], batch, local_rank, stream, args) if extras else None
         c3 = c3_leg(args, local_rank, stream) if extras and not args.no_c3 and args.config != "c3" else None
+        cluster = cluster_leg(local_rank) if extras and not args.no_cluster else None
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -300,6 +309,7 @@ def main():
             "host_path": hostp,
             "write2_wire_path": wire,
             "producer_signing": signing,
+            "cluster_c5_proxy": cluster,
             "correct_vs_ground_truth": all_ok,
             "cpu_baseline": cpu,
             "wall_s": round(wall_max, 4),
@@ -315,6 +325,8 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if getattr(args, "native_child", None) is not None and args.native_child.poll() is None:
+        args.native_child.kill()  # the wire leg never wrote its input
     ver.close()
 
 
@@ -426,6 +438,7 @@ def wire_path(ver, synth, R, strict, dev, stream, args):
                   for vs in ([ver], [ver, ver2]) for th in (2, 20)]
     async_leg = batcher_async_leg([ver, ver2], wb, synth.batch.cert_grant_off, R, strict, host)
     ver2.close()
+    native = batcher_native_leg(args, wb, R, host, synth.batch.cert_grant_off)
     return {"grants_per_s": round(N / t, 1), "ms_per_step": round(t * 1e3, 4), "messages": wb.n_msgs,
             "wire_bytes": int(wb.wire.nbytes), "verdicts_equal_soa_path": same,
             "host_encode_s": round(enc_s, 2),
@@ -435,7 +448,7 @@ def wire_path(ver, synth, R, strict, dev, stream, args):
                                     "verdicts_equal": host_same,
                                     "note": "mochi_verify_write2: pageable wire bytes staged + chunked H2D / decode+"
                                             "verify / D2H pipeline; device-event span, wall includes host staging"},
-            "batcher": batch_legs, "batcher_async": async_leg}
+            "batcher": batch_legs, "batcher_async": async_leg, "batcher_native": native}
 
 
 def batcher_leg(vers, wb, cert_grant_off, R, strict, threads, ref, max_msgs=4096, max_wait_us=100, n_req=20000):
@@ -541,6 +554,146 @@ def batcher_async_leg(vers, wb, cert_grant_off, R, strict, ref, n_req=100000, wi
             "gpu_batches": nb - nb0, "mean_batch_msgs": round((nm - nm0) / max(1, nb - nb0), 1),
             "verdicts_equal_one_shot": bool(np.array_equal(reasons, ref.cert_reason[:M])),
             "note": "one Python producer thread (ctypes call + callback per request bound the rate)"}
+
+
+NATIVE_CONFIGS = ["sync:2:1::20000", "sync:20:1::40000", "sync:20:2::40000", "sync:64:2::100000",
+                  "async:4:2:16384:400000"]
+
+
+def start_batcher_native(args, input_path):
+    """microbench/batcher_load: native threads calling mochi_batcher_verify (2, 20
+    and 64 of them -- the reference's worker pool is core 2 / max 20,
+    MochiServer.java:36-40) and an event-loop form on mochi_batcher_submit, over
+    real Write2ToServer bodies.  Started before this process uses the GPU; it
+    waits for `input_path`."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "microbench", "batcher_load")
+    if not os.path.exists(exe):
+        return None
+    os.makedirs(args.cache_dir, exist_ok=True)
+    cfgs = [c.replace("::", ":8192:") for c in NATIVE_CONFIGS]
+    return subprocess.Popen([exe, input_path, "20000", "4096", "100"] + cfgs, stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+
+
+def write_native_input(path, wb, R, ref):
+    """The driver's input (format in microbench/batcher_load.cpp): keys, server ids,
+    the Write2ToServer bodies and the expected verdict of each (the device one-shot
+    path's, itself equal to the oracle's in tests/test_write2_wire_gpu.py)."""
+    import struct
+
+    import numpy as np
+
+    import mochi_hip as mh
+    import workload as W
+
+    ids, id_off = W.server_id_table(R)
+    moduli = b"".join(mh.pem_modulus(p) for p in W.load_keys(R))
+    M = wb.n_msgs
+    off = np.ascontiguousarray(wb.msg_off, np.uint64)
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(b"MOCHIW2\0" + struct.pack("<II", R, M) + moduli)
+        f.write(struct.pack("<I", ids.nbytes) + ids.tobytes() + np.ascontiguousarray(id_off, np.uint32).tobytes())
+        f.write(struct.pack("<Q", wb.wire.nbytes) + wb.wire.tobytes() + off.tobytes())
+        f.write(np.ascontiguousarray(wb.msg_len, np.uint32).tobytes() + np.ascontiguousarray(wb.expected_hash).tobytes())
+        f.write(ref.cert_reason[:M].astype(np.uint8).tobytes() + ref.cert_accept[:M].astype(np.uint8).tobytes())
+    os.replace(tmp, path)
+
+
+def batcher_native_leg(args, wb, R, ref, cert_grant_off):
+    child = getattr(args, "native_child", None)
+    if child is None:
+        return None
+    try:
+        write_native_input(args.native_input, wb, R, ref)
+        out, err = child.communicate(timeout=600)
+    except Exception as ex:  # reported, never required
+        child.kill()
+        return {"error": f"batcher_load failed: {ex}"}
+    finally:
+        if os.path.exists(args.native_input):
+            os.remove(args.native_input)
+    rows = []
+    for line in out.splitlines():
+        try:
+            r = json.loads(line)
+        except ValueError:
+            continue
+        r["grants_per_s"] = round(r["requests_per_s"] * float(cert_grant_off[-1]) / max(1, len(cert_grant_off) - 1), 1)
+        rows.append(r)
+    res = {"rows": rows, "messages": wb.n_msgs, "rc": child.returncode,
+           "verdicts_equal_one_shot": bool(rows) and all(r["verdict_mismatches"] == 0 for r in rows),
+           "note": "microbench/batcher_load: native threads, no Python on the request path; request i sends "
+                   "message i % M; max_msgs 4096, max_wait 100 us"}
+    if child.returncode not in (0, 3):
+        res["stderr"] = err[-2000:]
+    return res
+
+
+def cluster_leg(dev, clients=256, txns_per_client=8, keys=2000, seed=11, backend="device"):
+    """In-process 4-server cluster from the reference's config/sample_config
+    (tests/cluster_harness.py) under a write-heavy multi-client KV load -- the C5
+    configuration's proxy (no JVM here): every Write1 grant signed on the device
+    (k_rsa_sign), Write1 rounds classified and responses tallied on the device,
+    every Write2 certificate verified through the batcher's request API with the
+    receiving server's stored state, its per-op decisions applied to the model.
+    Reports transactions/s and per-transaction latency (Write1 -> result)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import cluster_harness as H
+
+    c = H.Cluster(backend=backend, seed=seed, device=dev, max_wait_us=50)
+    rng = np.random.default_rng(seed)
+    t_done, lat, errors = [], [], []
+    n_reads = [0]
+
+    def script(cl):
+        import time as _t
+        written = []
+        for j in range(txns_per_client):
+            t0 = _t.perf_counter()
+            try:
+                if written and rng.random() < 0.1:  # read back a key this client wrote (a never-written key
+                    # has no container on the servers: processRead throws, the reference client hangs)
+                    r = yield ("read", H.read_ops(written[int(rng.integers(0, len(written)))]))
+                    n_reads[0] += 1
+                else:
+                    nk = 1 if rng.random() < 0.7 else 2
+                    ks = sorted({f"DEMO_KEY_STRESS_TEST_{int(x)}" for x in rng.integers(0, keys, nk)})
+                    r = yield ("write", H.write_ops(*[(k, f"v{cl.id}-{j}") for k in ks]))
+                    written.extend(ks)
+            except H.ClientError as ex:  # the reference client's exception for this transaction
+                errors.append(type(ex).__name__)
+                continue
+            lat.append(_t.perf_counter() - t0)
+
+    # warm the contexts (first launches, buffer sizing)
+    H.run_clients(c, [H.ScriptedClient(c, lambda cl: (yield ("write", H.write_ops(("WARM", "x")))))])
+    st0 = dict(c.stats)
+    t0 = time.perf_counter()
+    cl = [H.ScriptedClient(c, script) for _ in range(clients)]
+    try:
+        H.run_clients(c, cl)
+    except H.Hung as ex:
+        errors.append(str(ex))
+    wall = time.perf_counter() - t0
+    st = {k: c.stats[k] - st0.get(k, 0) for k in c.stats}
+    nb, nm = c.batcher.stats() if c.batcher else (0, 0)
+    c.close()
+    ls = np.sort(np.asarray(lat)) * 1e3 if lat else np.zeros(1)
+    n = len(lat)
+    return {"clients": clients, "transactions": n, "reads": n_reads[0], "transactions_per_s": round(n / wall, 1),
+            "write2_verifies_per_s": round(st["write2"] / wall, 1), "grants_signed_per_s": round(st["signed"] / wall, 1),
+            "latency_ms": {"p50": round(float(np.percentile(ls, 50)), 2), "p99": round(float(np.percentile(ls, 99)), 2)},
+            "write1_retries": st["retries"], "read_branch_ops": st["read_branch"], "scheduler_steps": st["steps"],
+            "client_errors": errors[:8], "n_client_errors": len(errors), "batcher_batches": nb,
+            "mean_batch_msgs": round(nm / max(1, nb), 1),
+            "note": "R=4 replicas of config/sample_config, 90% writes (70% 1-key, 30% 2-key), 10% reads over "
+                    f"{keys} keys; deterministic scheduler delivering random subsets of in-flight messages per step; "
+                    "wall clock includes the Python server/client models"}
 
 
 def wire_pipelined(ver, dwb, R, strict, dev, args, N, ref_host):

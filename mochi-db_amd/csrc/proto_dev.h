@@ -210,17 +210,38 @@ __device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_
   return true;
 }
 
-__device__ __noinline__ bool parse_grant_deep(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
-                                              uint32_t& oid_off, uint32_t& oid_len) {
+// The rare > 16-deep case, out of line.  Everything crosses the call by value
+// (the bytes' address and length in, the fields back in a struct): a reader or
+// output passed by reference would pin the caller's copies to the scratch
+// stack for the whole kernel, so the fast path's every byte read would go
+// through scratch memory.
+struct GrantFields {
+  int64_t ts;
+  uint32_t hash_off, hash_len, oid_off, oid_len;
+  uint32_t ok;
+};
+
+__device__ __noinline__ GrantFields parse_grant_deep(const uint8_t* p, uint32_t len) {
+  ByteReader r;
+  r.init(p, len);
+  GrantFields f{0, 0, 0, 0, 0, 0};
   bool unused = false;
-  return parse_grant_t<kDeepGroupDepth>(r, ts, hash_off, hash_len, oid_off, oid_len, unused);
+  f.ok = parse_grant_t<kDeepGroupDepth>(r, f.ts, f.hash_off, f.hash_len, f.oid_off, f.oid_len, unused) ? 1u : 0u;
+  return f;
 }
 
 __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
                                    uint32_t& oid_len) {
   bool too_deep = false;
   if (parse_grant_t<kMaxGroupDepth>(r, ts, hash_off, hash_len, oid_off, oid_len, too_deep)) return true;
-  return too_deep && parse_grant_deep(r, ts, hash_off, hash_len, oid_off, oid_len);
+  if (!too_deep) return false;
+  const GrantFields f = parse_grant_deep(r.base, r.len);
+  ts = f.ts;
+  hash_off = f.hash_off;
+  hash_len = f.hash_len;
+  oid_off = f.oid_off;
+  oid_len = f.oid_len;
+  return f.ok != 0;
 }
 
 __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
