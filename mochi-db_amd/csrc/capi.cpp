@@ -179,7 +179,8 @@ int make_fold_key(const uint8_t* n_be, mochi::FoldKey* f) {
   uint8_t le[264];
   for (int k = 0; k < kK && ok; k++) {
     if (k) ok = BN_lshift(r, r, (k & 3) ? 8 : 4) && BN_mod(r, r, n, ctx);  // limb = 8 + 8 + 8 + 4 bits
-    ok = ok && BN_add(sum, sum, r) && BN_bn2lebinpad(r, le, sizeof le) == (int)sizeof le;
+    if ((k & 3) != 3) ok = ok && BN_add(sum, sum, r);  // bytes 0..2 are biased, byte 3 is a signed digit
+    ok = ok && BN_bn2lebinpad(r, le, sizeof le) == (int)sizeof le;
     int carry = 0;
     for (int row = 0; row < kRows && ok; row++) {
       const int bit = 28 * (row >> 2) + 8 * (row & 3), w = (row & 3) == 3 ? 4 : 8;
@@ -191,7 +192,8 @@ int make_fold_key(const uint8_t* n_be, mochi::FoldKey* f) {
     }
     ok = ok && carry == 0;
   }
-  // cadd = 128 * sum R_{j,b} and cnc = cadd + n - Cpad (k_rsa_final) as 74 limbs of 28 bits
+  // cadd = 128 * sum_{j, b<3} R_{j,b} + kFoldOffN * n (fold.h) and cnc = cadd + n - Cpad
+  // (k_rsa_final) as 74 limbs of 28 bits
   auto limbs = [&](const BIGNUM* v, uint32_t* out) {
     if (BN_num_bits(v) > kLimbBits * kFoldLimbs || BN_bn2lebinpad(v, le, sizeof le) != (int)sizeof le) return 0;
     for (int q = 0; q < kFoldLimbs; q++) {
@@ -205,7 +207,10 @@ int make_fold_key(const uint8_t* n_be, mochi::FoldKey* f) {
   uint8_t cpad[256];
   pkcs1_cpad(cpad);
   BIGNUM* cp = BN_bin2bn(cpad, 256, nullptr);
-  ok = ok && cp && BN_lshift(sum, sum, 7) && limbs(sum, f->cadd);
+  BIGNUM* off = BN_new();
+  ok = ok && cp && off && BN_lshift(sum, sum, 7) && BN_set_word(off, kFoldOffN) && BN_mul(off, off, n, ctx) &&
+       BN_add(sum, sum, off) && limbs(sum, f->cadd);
+  BN_free(off);
   ok = ok && BN_add(sum, sum, n) && BN_sub(sum, sum, cp) && !BN_is_negative(sum) && limbs(sum, f->cnc);
   BN_free(cp);
   BN_free(n);

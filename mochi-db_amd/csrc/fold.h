@@ -25,11 +25,20 @@ constexpr int kFoldMT = 10;   // M-tiles (8 output limbs each)
 constexpr int kFoldImgBytes = kFoldMT * kFoldKS * 64 * 16;  // 102,400 B (one CU's LDS holds one key)
 constexpr int kFoldLimbs = 74;
 constexpr uint32_t kBucketAlign = 512;  // k_rsa_pow block = 8 waves of one signer
+// The fold's signed B operand: every t_hi limb is an int32 whose bytes 0..2 are
+// biased to signed (XOR 0x80: byte - 128) and whose byte 3 is taken as a signed
+// digit as it is, so a limb may be negative (kara_dev.h leaves t[37..111]
+// signed).  cadd adds the bias back (128 * sum_{j, b<3} R_{j,b}) plus
+// kFoldOffN * n, which keeps x' positive: every top digit is >= -32 (|t_j| <
+// 2^29) and t_lo > -n.  Then 0 < x' < 2^2064 (tests/fold_model.py).
+constexpr uint32_t kFoldBias = 0x00808080u;
+constexpr int kFoldOffN = 2401;
 
 struct FoldKey {
   int8_t img[kFoldImgBytes];
-  // the -128 bias of every t_hi byte removes 128 * R_{j,b} per K slot: cadd =
-  // 128 * sum R_{j,b} (< 2^2064), added back once as 74 normalised limbs
+  // the -128 bias of t_hi bytes 0..2 removes 128 * R_{j,b} per such K slot:
+  // cadd = 128 * sum_{j, b<3} R_{j,b} + kFoldOffN * n (< 2^2064), added back
+  // once as 74 normalised limbs
   uint32_t cadd[kFoldLimbs];
   // k_rsa_final's constant: cadd + n - Cpad (Cpad = the EMSA-PKCS1-v1_5
   // encoding with a zero digest), so its fold yields x + n - EM + H directly

@@ -19,6 +19,7 @@
 // odd" limbs.  A fragments are read from LDS (the key's image) one K-step ahead.
 #pragma once
 #include "fold.h"
+#include "kara_dev.h"
 #include "mont.h"
 
 namespace mochi {
@@ -48,8 +49,10 @@ constexpr int kHL = 10;  // a SHA-256 digest in radix 2^28
 typedef __attribute__((address_space(1))) char gchar;
 typedef __attribute__((address_space(1))) uint32_t guint;
 
-// BIASED: t_hi limbs (t[kFoldF..]) arrive already XOR 0x80808080.
-template <bool SUB_H, bool BIASED = false>
+// BIASED: t_hi limbs (t[kFoldF..]) arrive already XOR kFoldBias.
+// SIGNED_LO: t_lo limbs from kSignedLo (37) on are signed int32 (kara_dev.h)
+// and join the 64-bit carry chain on their own instead of the int32 sum.
+template <bool SUB_H, bool BIASED = false, bool SIGNED_LO = false>
 __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_t (&x)[kL],
                                             const v4i* __restrict__ wl, cptr cadd, const uint32_t* hl) {
   // tile 0's first A fragment: issued before the B operands are formed (their
@@ -63,9 +66,9 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
     static_for<0, 4>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       constexpr int jp = 8 * s + i, jq = 8 * s + 4 + i;
-      int p = (int)0x80808080u, q = (int)0x80808080u;
-      if constexpr (jp < kFoldNH) p = (int)(BIASED ? t[kFoldF + jp] : t[kFoldF + jp] ^ 0x80808080u);
-      if constexpr (jq < kFoldNH) q = (int)(BIASED ? t[kFoldF + jq] : t[kFoldF + jq] ^ 0x80808080u);
+      int p = 0, q = 0;  // padding K slots: their weights are zero
+      if constexpr (jp < kFoldNH) p = (int)(BIASED ? t[kFoldF + jp] : t[kFoldF + jp] ^ kFoldBias);
+      if constexpr (jq < kFoldNH) q = (int)(BIASED ? t[kFoldF + jq] : t[kFoldF + jq] ^ kFoldBias);
       swap32(p, q);  // p: N-tile 0 (signatures 0..31), q: N-tile 1 (32..63)
       b0[s][i] = p;
       b1[s][i] = q;
@@ -106,14 +109,18 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
       constexpr int q = 8 * mt + r, u = r >> 1;
       if constexpr (q < kL) {
         // limb q = c0 + 2^8 c1 + 2^16 (c2 + 2^8 c3) + t_lo + cadd (- h) + carry;
-        // the first terms of p stay in int32 (|c0 + 2^8 c1| < 1.27e9, t_lo, cadd
-        // and h < 2^28), h * 2^16 + p + carry is two v_mad_i64_i32
+        // the first terms of p stay in int32 (|c0 + 2^8 c1| < 1.27e9, normalised
+        // t_lo, cadd and h < 2^28), h * 2^16 + p + carry is two v_mad_i64_i32
+        // (three for a signed t_lo limb, up to +-2^29, which could overflow p)
+        constexpr bool lo_signed = SIGNED_LO && q >= kSignedLo && q < kFoldF;
         int p = (r & 1) ? p1[u] : p0[u];
-        if constexpr (q < kFoldF) p += (int)t[q];
+        if constexpr (q < kFoldF && !lo_signed) p += (int)t[q];
         p += (int)cadd[q];
         if constexpr (SUB_H && q < kHL) p -= (int)hl[q];
         const int h = (r & 1) ? h1[u] : h0[u];
-        const int64_t v = mad_i64(h, 65536, mad_i64(p, 1, carry));
+        int64_t c = carry;
+        if constexpr (lo_signed) c = mad_i64((int)t[q], 1, c);
+        const int64_t v = mad_i64(h, 65536, mad_i64(p, 1, c));
         x[q] = (uint32_t)v & kLimbMask;
         carry = v >> kLimbBits;
       }

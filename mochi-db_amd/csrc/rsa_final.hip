@@ -3,8 +3,9 @@
 // product and one matrix-core fold per grant.
 //
 // k_rsa_pow leaves z = s^(2^16) (mod n), z < 2^2064.  Then per grant
-//   t = z * s                                  148 limbs, VALU product scanning
-//                                              (74 x 74 = 5,476 v_mad_u64_u32)
+//   t = z * s                                  148 limbs, VALU, one level of
+//                                              Karatsuba (3 x 37 x 37 = 4,107
+//                                              v_mad_u64_u32, kara_dev.h)
 //   D = t_lo + fold(t_hi) + (n - Cpad) - H     the fold of k_rsa_pow (fold_dev.h)
 //                                              with the per-key constant
 //                                              cnc = cadd + n - Cpad
@@ -69,28 +70,9 @@ __device__ __forceinline__ void final_slot(uint32_t slot, uint32_t base, uint32_
       asm volatile("" : "+s"(zp));  // a running pointer: 74 limb bases would sit in SGPRs and spill
     }
   }
-  // ---- t = z * s: product scanning, two accumulators per column ----
+  // ---- t = z * s: one level of Karatsuba (kara_dev.h), t_hi biased ----
   uint32_t t[2 * kL];
-  {
-    uint64_t carry = 0;
-    static_for<0, 2 * kL - 1>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      constexpr int lo = k - kL + 1 > 0 ? k - kL + 1 : 0;
-      constexpr int hi = k < kL - 1 ? k : kL - 1;
-      uint64_t a0 = carry, a1 = 0;
-      static_for<lo, hi + 1>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i & 1) a1 = mad64(x[i], sv[k - i], a1);
-        else a0 = mad64(x[i], sv[k - i], a0);
-      });
-      const uint64_t acc = a0 + a1;
-      t[k] = (uint32_t)acc & kLimbMask;
-      asm volatile("" : "+v"(t[k]));  // materialise the 28-bit limb
-      carry = acc >> kLimbBits;
-      __builtin_amdgcn_sched_barrier(0);  // column by column (see fold_sqr)
-    });
-    t[2 * kL - 1] = (uint32_t)carry;
-  }
+  kara_product<false>(x, sv, t);
   // digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
   uint32_t hl[kHL];
   {
@@ -105,7 +87,7 @@ __device__ __forceinline__ void final_slot(uint32_t slot, uint32_t base, uint32_
     }
   }
   // ---- D = t_lo + fold(t_hi) + cadd + n - Cpad - H ----
-  fold_reduce<true>(t, x, w + (threadIdx.x & 63), as_const(fold[key].cnc), hl);
+  fold_reduce<true, true, true>(t, x, w + (threadIdx.x & 63), as_const(fold[key].cnc), hl);
   // ---- D' = (D + m n) / 2^28 == n ? ----
   cptr nn = n;
   asm volatile("" : "+s"(nn));  // reload n here (kept from the s < n check it would sit in SGPRs and spill)

@@ -2,7 +2,8 @@
 // (z < 2^2064, not fully reduced), one signature per lane, with the modular
 // reduction on the matrix cores (fold.h):
 //
-//   per squaring   t = x^2          VALU product scanning, 2,775 v_mad_u64_u32
+//   per squaring   t = x^2          VALU, one level of Karatsuba over three
+//                                   37-limb squares: 2,109 v_mad_u64_u32 (kara_dev.h)
 //                  x = t_lo + W t_hi  v_mfma_i32_32x32x32_i8, 10 M-tiles x 10 K-steps
 //                                   x 2 N-tiles (the wave's 64 signatures)
 //
@@ -27,115 +28,10 @@
 namespace mochi {
 namespace {
 
-#ifndef MOCHI_SQR
-#define MOCHI_SQR 1
-#endif
-
-// column k of x^2: cross products x_i x_{k-i}, i in [sq_lo(k), sq_hi(k)]
-constexpr int sq_lo(int k) { return k - kL + 1 > 0 ? k - kL + 1 : 0; }
-constexpr int sq_hi(int k) { return k > 0 ? (k - 1) / 2 : -1; }
-constexpr int sq_len(int k) { return sq_hi(k) - sq_lo(k) + 1 > 0 ? sq_hi(k) - sq_lo(k) + 1 : 0; }
-
 __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restrict__ wl, cptr cadd) {
-  // ---- t = x^2: product scanning, cross products once, column sum doubled ----
   uint32_t t[2 * kL];
-#if MOCHI_SQR == 4
-  // four columns at a time (four independent accumulation chains)
-  {
-    uint64_t carry = 0;
-    static_for<0, kL / 2 + 1>([&](auto pc) {
-      constexpr int kb = 4 * decltype(pc)::value;
-      constexpr int nq0 = kb < 2 * kL ? sq_len(kb) : 0, nq1 = kb + 1 < 2 * kL ? sq_len(kb + 1) : 0;
-      constexpr int nq2 = kb + 2 < 2 * kL ? sq_len(kb + 2) : 0, nq3 = kb + 3 < 2 * kL ? sq_len(kb + 3) : 0;
-      constexpr int nmax = nq0 > nq1 ? (nq0 > nq2 ? (nq0 > nq3 ? nq0 : nq3) : (nq2 > nq3 ? nq2 : nq3))
-                                     : (nq1 > nq2 ? (nq1 > nq3 ? nq1 : nq3) : (nq2 > nq3 ? nq2 : nq3));
-      uint64_t c[4] = {0, 0, 0, 0};
-      static_for<0, nmax>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        static_for<0, 4>([&](auto jc) {
-          constexpr int j = decltype(jc)::value, k = kb + j;
-          constexpr int n = j == 0 ? nq0 : j == 1 ? nq1 : j == 2 ? nq2 : nq3;
-          if constexpr (i < n) c[j] = mad64(x[sq_lo(k) + i], x[k - sq_lo(k) - i], c[j]);
-        });
-      });
-      static_for<0, 4>([&](auto jc) {
-        constexpr int j = decltype(jc)::value, k = kb + j;
-        if constexpr (k < 2 * kL - 1) {
-          asm("" : "+v"(c[j]));
-          uint64_t acc = carry + (c[j] << 1);
-          if constexpr ((k & 1) == 0) acc = mad64(x[k >> 1], x[k >> 1], acc);
-          t[k] = k < kFoldF ? (uint32_t)acc & kLimbMask : ((uint32_t)acc & kLimbMask) ^ 0x80808080u;
-          asm volatile("" : "+v"(t[k]));
-          carry = acc >> kLimbBits;
-        } else if constexpr (k == 2 * kL - 1) {
-          t[k] = (uint32_t)carry ^ 0x80808080u;
-        }
-      });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-#elif MOCHI_SQR == 1
-  // two columns at a time: their cross-product chains are independent, so the
-  // mads interleave (one accumulation chain per column would issue each mad
-  // behind its predecessor's result, and the 64-bit chain result is read by
-  // the carry step one wait state later)
-  {
-    uint64_t carry = 0;
-    static_for<0, kL>([&](auto pc) {
-      constexpr int k0 = 2 * decltype(pc)::value, k1 = k0 + 1;
-      constexpr int n0 = sq_len(k0), n1 = sq_len(k1), nmax = n0 > n1 ? n0 : n1;
-      uint64_t c0 = 0, c1 = 0;
-      static_for<0, nmax>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i < n0) c0 = mad64(x[sq_lo(k0) + i], x[k0 - sq_lo(k0) - i], c0);
-        if constexpr (i < n1) c1 = mad64(x[sq_lo(k1) + i], x[k1 - sq_lo(k1) - i], c1);
-      });
-      asm("" : "+v"(c0));  // double each column sum once
-      asm("" : "+v"(c1));
-      uint64_t acc = mad64(x[k0 >> 1], x[k0 >> 1], carry + (c0 << 1));
-      t[k0] = k0 < kFoldF ? (uint32_t)acc & kLimbMask : ((uint32_t)acc & kLimbMask) ^ 0x80808080u;
-      asm volatile("" : "+v"(t[k0]));
-      carry = acc >> kLimbBits;
-      if constexpr (k1 < 2 * kL - 1) {
-        acc = carry + (c1 << 1);
-        t[k1] = k1 < kFoldF ? (uint32_t)acc & kLimbMask : ((uint32_t)acc & kLimbMask) ^ 0x80808080u;
-        asm volatile("" : "+v"(t[k1]));
-        carry = acc >> kLimbBits;
-      } else {
-        t[k1] = (uint32_t)carry ^ 0x80808080u;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-#else
-  {
-    uint64_t carry = 0;
-    static_for<0, 2 * kL - 1>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      constexpr int lo = k - kL + 1 > 0 ? k - kL + 1 : 0;
-      constexpr int xhi = k > 0 ? (k - 1) / 2 : -1;
-      uint64_t x0 = 0, x1 = 0;
-      static_for<lo, xhi + 1>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i & 1) x1 = mad64(x[i], x[k - i], x1);
-        else x0 = mad64(x[i], x[k - i], x0);
-      });
-      uint64_t xs = x0 + x1;
-      asm("" : "+v"(xs));  // double the column sum once (else hipcc doubles every x_i: extra mads and registers)
-      uint64_t acc = carry + (xs << 1);
-      if constexpr ((k & 1) == 0) acc = mad64(x[k >> 1], x[k >> 1], acc);
-      // t_hi limbs leave here already biased for the fold's signed B operand
-      t[k] = k < kFoldF ? (uint32_t)acc & kLimbMask : ((uint32_t)acc & kLimbMask) ^ 0x80808080u;
-      asm volatile("" : "+v"(t[k]));  // materialise the 28-bit limb (else the 64-bit column stays live)
-      carry = acc >> kLimbBits;
-      // column by column: left alone the scheduler hoists later columns' mads
-      // and keeps ~40 64-bit column sums live
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    t[2 * kL - 1] = (uint32_t)carry ^ 0x80808080u;
-  }
-#endif
-  fold_reduce<false, true>(t, x, wl, cadd, nullptr);
+  kara_product<true>(x, x, t);                // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
+  fold_reduce<false, true, true>(t, x, wl, cadd, nullptr);
 }
 
 // Persistent: one block per CU walks a contiguous range of 512-slot groups, so

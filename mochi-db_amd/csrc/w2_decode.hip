@@ -75,49 +75,58 @@ __device__ __forceinline__ bool vlen(ByteReader& r, uint32_t& pos, uint32_t end,
 }
 
 // Skip an unknown group opened by `field` (skipMessage + checkLastTagWas).
-// Rare: kept out of line so its stack does not weigh on the common path.
-__device__ __noinline__ bool skip_group(ByteReader& r, uint32_t& pos, uint32_t end, uint32_t field) {
+// Rare: kept out of line so its stack does not weigh on the common path, and
+// called with plain values -- a reader or position passed by reference would
+// pin the callers' copies to the scratch stack, and every byte the common path
+// reads would then go through scratch.  Returns the position after the group,
+// or kSkipBad.
+constexpr uint32_t kSkipBad = 0xFFFFFFFFu;
+
+__device__ __noinline__ uint32_t skip_group(const uint8_t* base, uint32_t len, uint32_t pos, uint32_t end,
+                                            uint32_t field) {
+  ByteReader r;
+  r.init(base, len);
   uint32_t stack[kDeepGroupDepth];
   int depth = 1;
   stack[0] = field;
 #pragma unroll 1
   while (depth > 0) {
     uint64_t t64;
-    if (!vint(r, pos, end, t64)) return false;
+    if (!vint(r, pos, end, t64)) return kSkipBad;
     const uint32_t t = (uint32_t)t64, f = t >> 3, wt = t & 7;
-    if (f == 0) return false;
+    if (f == 0) return kSkipBad;
     uint32_t l;
     switch (wt) {
       case 0: {
         uint64_t v;
-        if (!vint(r, pos, end, v)) return false;
+        if (!vint(r, pos, end, v)) return kSkipBad;
         break;
       }
       case 1:
-        if (end - pos < 8) return false;
+        if (end - pos < 8) return kSkipBad;
         pos += 8;
         break;
       case 2:
-        if (!vlen(r, pos, end, l)) return false;
+        if (!vlen(r, pos, end, l)) return kSkipBad;
         pos += l;
         break;
       case 3:
-        if (depth >= kDeepGroupDepth) return false;
+        if (depth >= kDeepGroupDepth) return kSkipBad;
         stack[depth++] = f;
         break;
       case 4:
-        if (stack[depth - 1] != f) return false;
+        if (stack[depth - 1] != f) return kSkipBad;
         depth--;
         break;
       case 5:
-        if (end - pos < 4) return false;
+        if (end - pos < 4) return kSkipBad;
         pos += 4;
         break;
       default:
-        return false;
+        return kSkipBad;
     }
   }
-  return true;
+  return pos;
 }
 
 // Next field in [pos, end): 1 field, 0 end, -1 malformed.
@@ -143,8 +152,12 @@ __device__ int next_fld(ByteReader& r, uint32_t& pos, uint32_t end, Fld& f) {
       f.off = pos;
       pos += f.len;
       return 1;
-    case 3:
-      return skip_group(r, pos, end, f.field) ? 1 : -1;
+    case 3: {
+      const uint32_t np = skip_group(r.base, r.len, pos, end, f.field);
+      if (np == kSkipBad) return -1;
+      pos = np;
+      return 1;
+    }
     case 5:
       if (end - pos < 4) return -1;
       pos += 4;

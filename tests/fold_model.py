@@ -16,6 +16,11 @@ This module builds the weight image in the exact per-lane MFMA fragment order
 and replays the arithmetic with Python ints.  Checked against the library's
 mochi_fold_matrix and against pow() in tests/test_fold_cpu.py.
 """
+# Round 3: the product is one level of Karatsuba (kara_terms) and leaves the
+# limbs 37..111 signed and unnormalised; the fold takes each t_hi limb as an
+# int32 whose low three bytes are biased (XOR 0x80) and whose top byte is a
+# signed digit, and cadd carries 128 * sum_{j, b<3} R_{j,b} + 2401 n (the
+# multiple of n keeps x' > 0 whatever the signs).
 import numpy as np
 
 L = 74          # limbs of x (2072 bits)
@@ -41,6 +46,17 @@ def balanced_digits(v):
     return d
 
 
+HALF = 37        # Karatsuba split: x = x_lo + 2^(28*37) x_hi
+BIAS_MASK = 0x00808080  # t_hi bytes 0..2 biased to signed, byte 3 a signed digit
+OFF_N = 2401     # cadd's multiple of n: top digits >= -32 (|t_j| < 2^29) and t_lo > -n
+
+
+def cadd_value(n):
+    """sum_{j, b<3} 128 R_{j,b} + OFF_N n: the bias of bytes 0..2 added back, plus
+    a multiple of n that keeps x' positive whatever the signed limbs."""
+    return 128 * sum(pow(2, 28 * (F + j) + 8 * b, n) for j in range(NH) for b in range(3)) + OFF_N * n
+
+
 def make_weights(n):
     """Weight image int8 [MTILES][KSTEPS][64 lanes][16], cadd uint32 [74], W."""
     W = np.zeros((L * 4, NH * 4), np.int64)  # [out row (q,s)][k (j,b)]
@@ -58,12 +74,92 @@ def make_weights(n):
                     limb = 8 * ks + 4 * h + jj // 4
                     if row < L * 4 and limb < NH:
                         img[mt, ks, lane, jj] = W[row, 4 * limb + jj % 4]
-    # bias correction: sum_k 128 * R_k, added once as a normalised 74-limb number
-    # (the -128 bias of every t_hi byte removes exactly 128 * R_k per k)
-    ctot = 128 * sum(pow(2, 28 * (F + j) + 8 * b, n) for j in range(NH) for b in range(4))
+    ctot = cadd_value(n)
     assert ctot < 1 << (28 * L)
     cadd = np.array(to_limbs(ctot), np.uint32)
     return img, cadd, W
+
+
+def _columns(a, b, sqr):
+    """Product-scanning column sums of a*b (a*a with the cross products counted
+    once and doubled when sqr), normalised through the kernel's 64-bit carry chain."""
+    na = len(a)
+    out, carry = [], 0
+    for k in range(2 * na - 1):
+        lo, hi = max(0, k - na + 1), min(k, na - 1)
+        if sqr:
+            cross = sum(a[i] * a[k - i] for i in range(lo, (k - 1) // 2 + 1) if i < k - i)
+            assert cross < 1 << 64
+            acc = carry + 2 * cross + (a[k // 2] * a[k // 2] if k % 2 == 0 else 0)
+        else:
+            acc = carry + sum(a[i] * b[k - i] for i in range(lo, hi + 1))
+        assert acc < 1 << 64, "column sum overflows the 64-bit accumulator"
+        out.append(acc & M28)
+        carry = acc >> 28
+    out.append(carry & M28)
+    out.append(carry >> 28)
+    return out  # 2 na + 1 limbs (the last one is zero unless the operands exceed 28 bits)
+
+
+def kara_terms(a, b=None):
+    """t = a*b (a*a if b is None), 74-limb operands, as 148 signed limbs: the
+    kernel's one-level Karatsuba with its order of operations (M, then L, then H)
+    and no normalisation of the combination, t[37..111] in (-2^29, 2^29)."""
+    sqr = b is None
+    a0, a1 = list(a[:HALF]), list(a[HALF:])
+    if sqr:
+        S = [a0[i] + a1[i] for i in range(HALF)]
+        M = _columns(S, None, True)
+        Lw = _columns(a0, None, True)
+        Hw = _columns(a1, None, True)
+    else:
+        b0, b1 = list(b[:HALF]), list(b[HALF:])
+        M = _columns([a0[i] + a1[i] for i in range(HALF)], [b0[i] + b1[i] for i in range(HALF)], False)
+        Lw = _columns(a0, b0, False)
+        Hw = _columns(a1, b1, False)
+    assert len(M) == 75 and Lw[74] == 0 and Hw[74] == 0
+    t = [0] * (2 * L)
+    for k in range(75):          # M_k -> t[37 + k]
+        t[HALF + k] = M[k]
+    for k in range(74):          # L: t[k] (+)= L_k, t[37 + k] -= L_k
+        if k < HALF:
+            t[k] = Lw[k]
+        else:
+            t[k] += Lw[k]
+        t[HALF + k] -= Lw[k]
+    for m in range(74):          # H: t[37 + m] -= H_m, t[74 + m] (+)= H_m
+        t[HALF + m] -= Hw[m]
+        if m <= HALF:
+            t[2 * HALF + m] += Hw[m]
+        else:
+            t[2 * HALF + m] = Hw[m]
+    assert all(-(1 << 29) < v < (1 << 29) for v in t)
+    av, bv = from_limbs(a), from_limbs(a if sqr else b)
+    assert sum(v << (28 * k) for k, v in enumerate(t)) == av * bv
+    return t
+
+
+def fold_signed(t, W, cadd, sub_h=None):
+    """x' = t_lo + fold(t_hi) + cadd (- h): the kernel's fold of signed limbs."""
+    t_lo, t_hi = t[:F], t[F:]
+    kb = []
+    for j in range(NH):
+        v = t_hi[j] & 0xFFFFFFFF
+        for bb in range(4):
+            byte = (v >> (8 * bb)) & 0xFF
+            kb.append(byte - 128 if bb < 3 else (byte - 256 if byte >= 128 else byte))
+    c = (W @ np.array(kb, np.int64)).reshape(L, 4)
+    assert np.abs(c).max() < 2 ** 31
+    out, carry = [], 0
+    for q in range(L):
+        p = int(c[q, 0]) + (int(c[q, 1]) << 8) + int(cadd[q]) - (sub_h[q] if sub_h and q < len(sub_h) else 0)
+        h = int(c[q, 2]) + (int(c[q, 3]) << 8)
+        assert -2 ** 31 <= p < 2 ** 31 and -2 ** 31 <= h < 2 ** 31  # the kernel's int32 halves
+        v = (h << 16) + p + (t_lo[q] if q < F else 0) + carry
+        out.append(v & M28)
+        carry = v >> 28
+    assert carry == 0
+    return out
 
 
 def to_limbs(v, n=L):
@@ -75,23 +171,9 @@ def from_limbs(x):
 
 
 def fold_square(x, W, cadd):
-    """One step on limbs, the kernel's arithmetic exactly (int8 bias included)."""
-    xv = from_limbs(x)
-    t = to_limbs(xv * xv, 2 * L)
-    t_lo, t_hi = t[:F], t[F:]
-    kb = np.array([((t_hi[j] >> (8 * b)) & 0xFF) - 128 for j in range(NH) for b in range(4)], np.int64)
-    c = (W @ kb).reshape(L, 4)  # raw MFMA columns
-    assert np.abs(c).max() < 2 ** 31
-    out, carry = [], 0
-    for q in range(L):
-        p = int(c[q, 0]) + (int(c[q, 1]) << 8) + (t_lo[q] if q < F else 0) + int(cadd[q])
-        h = int(c[q, 2]) + (int(c[q, 3]) << 8)
-        assert -2 ** 31 <= p < 2 ** 31 and -2 ** 31 <= h < 2 ** 31  # the kernel's int32 halves
-        v = (h << 16) + p + carry
-        out.append(v & M28)
-        carry = v >> 28
-    assert carry == 0
-    return out
+    """One step on limbs, the kernel's arithmetic exactly (Karatsuba x^2, signed
+    limbs, int8 bias of bytes 0..2 included)."""
+    return fold_signed(kara_terms(x), W, cadd)
 
 
 def self_check(seed=1, iters=16):

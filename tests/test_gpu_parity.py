@@ -249,6 +249,12 @@ def test_large_batch_c3_bit_exact(pool7, ver7, strict):
     np.testing.assert_array_equal(g.grant_flags, s.expected_flags)
     o = _oracle_tally_own_parse(s.batch, g.grant_flags, s.expected_flags, 7, strict)
     assert_same_certs(g, o)
+    # the ground truth is pinned by OpenSSL too: 8 slices of 1000 grants across the batch
+    # (invalid signature => the grant is absent, InMemoryDataStore.java:622-624)
+    for lo in np.linspace(0, s.batch.n_grants - 1000, 8).astype(np.int64):
+        of, ot = O.verify_grants(pool7.moduli, s.batch, int(lo), int(lo) + 1000, 8)
+        np.testing.assert_array_equal(g.grant_flags[lo:lo + 1000], of[lo:lo + 1000])
+        np.testing.assert_array_equal(g.grant_ts[lo:lo + 1000], ot[lo:lo + 1000])
 
 
 def test_c4_16m_batch_bit_exact():
@@ -268,8 +274,14 @@ def test_c4_16m_batch_bit_exact():
     o = _oracle_tally_own_parse(b, g.grant_flags, s.expected_flags, R, True)
     assert_same_certs(g, o)
     assert (~g.cert_accept).sum() > 0.01 * C
-    # OpenSSL on 8 slices of 1000 grants across the batch
-    for lo in np.linspace(0, b.n_grants - 1000, 8).astype(np.int64):
+    # the device-signed stream is pinned by OpenSSL itself: the whole first 1M grants
+    # (16 threads), then 8 slices of 1000 grants across the rest of the batch
+    head = 1_000_000
+    of, ot = O.verify_grants(moduli_for(R), b, 0, head, 16)
+    np.testing.assert_array_equal(g.grant_flags[:head], of[:head])
+    np.testing.assert_array_equal(g.grant_ts[:head], ot[:head])
+    assert (of[:head] & mh.GRANT_SIG_OK).sum() < head  # the fault mix reaches the head
+    for lo in np.linspace(head, b.n_grants - 1000, 8).astype(np.int64):
         of, ot = O.verify_grants(moduli_for(R), b, int(lo), int(lo) + 1000, 8)
         np.testing.assert_array_equal(g.grant_flags[lo:lo + 1000], of[lo:lo + 1000])
     ver.close()
