@@ -18,6 +18,8 @@
 // rows 4h + 8u + 0..3 = limb 2u + h of the M-tile) back into "own even | own
 // odd" limbs.  A fragments are read from LDS (the key's image) one K-step ahead.
 #pragma once
+#include <atomic>
+
 #include "fold.h"
 #include "kara_dev.h"
 #include "mont.h"
@@ -158,17 +160,22 @@ __device__ __forceinline__ void for_groups(const uint32_t* __restrict__ perm, ui
   }
 }
 
-// one persistent 512-thread block per CU (the 100 KB image allows one per CU)
+// one persistent 512-thread block per CU (the 100 KB image allows one per CU).
+// The CU count is cached per device in atomics: several host threads launch
+// concurrently (batcher flushers, multi-GPU workers, pipelined contexts).
 inline uint32_t fold_grid(uint32_t n_slots) {
-  static int n_cu[64] = {0};
+  static std::atomic<int> n_cu[64];  // zero-initialised (static storage)
   int dev = 0;
   (void)hipGetDevice(&dev);
-  if (dev >= 0 && dev < 64 && n_cu[dev] == 0) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    n_cu[dev] = v;
+  uint32_t cus = 256u;
+  if (dev >= 0 && dev < 64) {
+    int v = n_cu[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
+      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+      n_cu[dev].store(v, std::memory_order_relaxed);  // every writer stores the same value
+    }
+    cus = (uint32_t)v;
   }
-  const uint32_t cus = dev >= 0 && dev < 64 ? (uint32_t)n_cu[dev] : 256u;
   const uint32_t groups = (n_slots + kBucketAlign - 1) / kBucketAlign;
   return groups < cus ? groups : cus;
 }

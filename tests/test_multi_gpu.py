@@ -73,3 +73,54 @@ def test_comm_single_rank_allgather():
     torch.cuda.synchronize()
     assert torch.equal(src, dst)
     c.close()
+
+
+def test_mverify_write2_rejects_grant_level_outputs(pool4):
+    """Like mochi_verify_write2 (check_write2_header), the multi-device wire path
+    produces no grant-level outputs and says so instead of leaving them unwritten."""
+    import ctypes
+
+    s = W.make_batch(pool4, 64, first_cert=77)
+    wb = W.encode_wire_batch(s)
+    mv = mh.MultiVerifier(pool4.moduli, _mask())
+    mv.set_server_ids(W.SERVER_IDS[:4])
+    wc, keep = mh.write2_batch_c(wb)
+    out = mh.Verdicts.alloc(s.batch.n_grants, wb.n_msgs, int(wb.op_flags_off[-1]))
+    vc = out.to_c()  # grant_flags / grant_ts / grant_valid_bits set
+    p = mh.params(4, True)
+    st = np.zeros(wb.n_msgs, np.uint8)
+    rc = mv.lib.mochi_mverify_write2(mv.h, ctypes.addressof(wc), ctypes.addressof(p), ctypes.addressof(vc),
+                                     st.ctypes.data)
+    assert rc == mh.EINVAL
+    assert b"grant-level" in mv.lib.mochi_last_error()
+    mv.close()
+
+
+def test_mctx_gathered_bits_are_the_verdicts(pool4):
+    """The all-gather reads each device's accept bitmap where the verify left it:
+    device 0's gathered buffer, assembled, equals the batch's verdict bitmap."""
+    s = W.make_batch(pool4, 4096 + 45, first_cert=5)  # a full 32-aligned shard plus a ragged tail
+    mv = mh.MultiVerifier(pool4.moduli, _mask())
+    g = mv.verify(s.batch, 4, True)
+    ptr, words = mv.gathered_bits(0)
+    n = len(mv.devices)
+    plan = mh.shard_plan(s.batch.n_certs, n, s.batch.cert_grant_off)
+    got = mh.bits_assemble(plan, _d2h(ptr, n * words))
+    np.testing.assert_array_equal(got[:g.cert_accept_bits.shape[0]], g.cert_accept_bits)
+    mv.close()
+
+
+def _d2h(dev_ptr, words):
+    """Copy `words` uint32 from a raw device pointer with the HIP runtime this
+    process already mapped (torch's and the library's)."""
+    import ctypes
+
+    import torch
+
+    torch.cuda.synchronize()
+    path = next(line.split()[-1] for line in open("/proc/self/maps") if "libamdhip64.so" in line)
+    hip = ctypes.CDLL(path)
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.zeros(words, np.uint32)
+    assert hip.hipMemcpy(out.ctypes.data, dev_ptr, 4 * words, 2) == 0  # hipMemcpyDeviceToHost
+    return out
