@@ -66,6 +66,29 @@ __device__ __forceinline__ bool rd_varint(ByteReader& r, uint32_t& pos, uint64_t
 
 __device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
   uint32_t i = 0;
+  // ASCII runs (keys, ids, the 128-char hex transactionHash) 32 bytes per step
+  // at any alignment: the 9 aligned words that hold the 32 bytes are loaded
+  // together (independent loads: one latency per step, not one per word) and
+  // every byte of the window is tested for its high bit.  Each word holds at
+  // least one byte of the window, which lies inside the string, so every load
+  // stays in bounds (as ByteReader::at's).  A window with a non-ASCII byte
+  // falls through to the byte-wise UTF-8 check below.
+#pragma unroll 1
+  while (i + 32 <= n) {
+    const uintptr_t a = r.abase + (uintptr_t)(off + i + r.shift);
+    const uint32_t* wp = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t w[9];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = wp[k];
+    w[8] = sh ? wp[8] : 0u;
+    uint32_t hi = w[0] & (0x80808080u << (8 * sh));
+#pragma unroll
+    for (int k = 1; k < 8; k++) hi |= w[k];
+    if (sh) hi |= w[8] & (0x80808080u >> (8 * (4 - sh)));
+    if (hi & 0x80808080u) break;
+    i += 32;
+  }
 #pragma unroll 1
   while (i < n) {
     // 16 ASCII bytes per step once the position is 16-byte aligned (all 16

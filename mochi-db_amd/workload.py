@@ -345,11 +345,15 @@ class WireBatch:
         return int(self.msg_off.shape[0])
 
 
-def encode_wire_batch(s: Synth, server_ids=None, client_id: str = "client-7f3a", pad: int = 0) -> WireBatch:
+def encode_wire_batch(s: Synth, server_ids=None, client_id: str = "", pad: int = 0, mg_hash: bool = False) -> WireBatch:
     """The Write2ToServer messages a MochiDB server would receive for the
     synthetic certificates of `s`: one MultiGrant per replica in server order
     (certificate map key = MultiGrant.serverId), grants keyed by objectId with
-    their signatures in grantSignatures, a WRITE operation per op key."""
+    their signatures in grantSignatures, a WRITE operation per op key.  As the
+    reference's producer builds them, MultiGrant.clientId is empty (it copies
+    Write1ToServer.clientId, which MochiDBClient never sets:
+    InMemoryDataStore.java:285, MochiDBClient.java:252-263) and MultiGrant.hash
+    is unset; client_id / mg_hash=True add them (decoder coverage)."""
     b = s.batch
     ids = server_ids or SERVER_IDS
     C = b.n_certs
@@ -375,7 +379,7 @@ def encode_wire_batch(s: Synth, server_ids=None, client_id: str = "client-7f3a",
         enc = []
         for r, items in mgs:
             sid = ids[r] if r < len(ids) else f"server-unknown-{r}"
-            mg = encode_multigrant([(o, gb) for o, gb, _ in items], sid, client_id, th,
+            mg = encode_multigrant([(o, gb) for o, gb, _ in items], sid, client_id, th if mg_hash else "",
                                    [(o, sg) for o, _, sg in items])
             enc.append((sid, mg))
         ops = [encode_operation(2, oids.get(int(b.op_key[o]), f"key-{int(b.op_key[o])}"), f"value-{c}-{o - o0}")

@@ -23,7 +23,7 @@ def pool4k2():
 def test_oracle_decode_roundtrip(pool4, pool4k2, which):
     pool = pool4 if which == "k1" else pool4k2
     s = W.make_batch(pool, 300, first_cert=41)
-    wb = W.encode_wire_batch(s, pad=3)
+    wb = W.encode_wire_batch(s, pad=3, client_id="client-7f3a", mg_hash=True)
     ids, off = W.server_id_table(4)
     d = O.w2_decode(wb, ids, off)
     b = s.batch

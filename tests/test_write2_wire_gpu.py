@@ -94,7 +94,7 @@ def test_device_decode_golden_vectors(pool4):
 def test_wire_verdicts_equal_soa_verdicts(pool4, strict):
     ver = _ver(pool4)
     s = W.make_batch(pool4, 3000, first_cert=321)
-    wb = W.encode_wire_batch(s, pad=5)
+    wb = W.encode_wire_batch(s, pad=5, client_id="client-7f3a", mg_hash=True)
     g, st = ver.verify_write2(wb, 4, strict)
     assert (st == 0).all()
     soa = ver.verify(s.batch, 4, strict)
