@@ -217,22 +217,27 @@ struct TallyArgs {
 };
 
 // MOCHI_Q_BIND: Grant.objectId == the op key it is filed under (op `o`'s
-// operand1) and Grant.transactionHash == expected.
-__device__ bool grant_bound(const TallyArgs& a, uint32_t g, uint32_t o, const uint8_t* expected) {
-  if (!a.op_key_off || !a.op_key_len) return false;
+// operand1) and Grant.transactionHash == expected.  Out of line and called with
+// plain values: the bind mode is rare, and its Grant parse inlined into k_tally
+// would cost every certificate of every mode registers.
+__device__ __noinline__ bool grant_bound_at(const uint8_t* gp, uint32_t glen, const uint8_t* k, uint32_t kl,
+                                            const uint8_t* expected) {
   ByteReader r;
-  r.init(a.blob + a.grant_off[g], a.grant_len[g]);
+  r.init(gp, glen);
   int64_t t;
   uint32_t ho, hl, oo, ol;
   if (!parse_grant(r, t, ho, hl, oo, ol)) return false;
-  const uint32_t kl = a.op_key_len[o];
   if (ol != kl) return false;
-  const uint8_t* k = a.blob + a.op_key_off[o];
-  const uint8_t* id = a.blob + a.grant_off[g] + oo;
+  const uint8_t* id = gp + oo;
 #pragma unroll 1
   for (uint32_t i = 0; i < kl; i++)
     if (id[i] != k[i]) return false;
-  return hash_matches(a.blob, a.grant_off[g] + ho, hl, expected);
+  return hash_matches(gp, ho, hl, expected);
+}
+
+__device__ __forceinline__ bool grant_bound(const TallyArgs& a, uint32_t g, uint32_t o, const uint8_t* expected) {
+  if (!a.op_key_off || !a.op_key_len) return false;
+  return grant_bound_at(a.blob + a.grant_off[g], a.grant_len[g], a.blob + a.op_key_off[o], a.op_key_len[o], expected);
 }
 
 // Grant g counts toward its key slot's quorum list (reference parity: its

@@ -560,16 +560,6 @@ __device__ bool valid_mg_count(ByteReader& r, uint32_t off, uint32_t len, uint32
   return rc == 0;
 }
 
-// Distinct grants of a decoded MultiGrant value, each canonical (else false).
-__device__ bool mg_distinct_canonical(ByteReader& r, uint32_t off, uint32_t len, uint32_t& ng) {
-  ng = 0;
-  return for_map(r, off, len, 1, [&](const Entry&, const Entry& gv) -> bool {
-    if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
-    ng++;
-    return true;
-  });
-}
-
 // Certificate entries (compact, in wire order per message): message index,
 // key and value slices (message-relative), the index of the entry holding the
 // key's final value (~0 unless this entry is the key's first), and the number
@@ -590,6 +580,70 @@ __host__ __device__ inline CE ce_view(uint32_t* p, uint32_t cap) {
 // The distinct grants of one decoded MultiGrant value [mo, mo+ml), in map
 // order: sink(grant value off, len, signer, signature off or ~0, key slot),
 // offsets message-relative.
+// One pass for k_w2_mg: the distinct grants of the decoded MultiGrant value,
+// each canonical (else false: fast-path exit), counted into ng; the first
+// one's emit record (grant slice, signer, signature offset, key slot) goes to
+// rec(...).  The map is
+// resolved once and the signature / key-slot lookups run for the first grant
+// only (k_w2_emit_mg redoes them for a MultiGrant with several grants).
+template <typename Rec>
+__device__ bool mg_decode_first(ByteReader& r, uint32_t mo, uint32_t ml, uint32_t tx_off, uint32_t tx_len,
+                                const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids,
+                                uint32_t& ng, Rec&& rec) {
+  ng = 0;
+  return for_map(r, mo, ml, 1, [&](const Entry& ge, const Entry& gv) -> bool {
+    if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
+    if (ng++ == 0) {
+      uint16_t signer = 0xFFFF;
+      {
+        uint32_t so, sl;
+        last_string(r, mo, ml, 4, so, sl);  // MultiGrant.serverId
+#pragma unroll 1
+        for (uint32_t k = 0; k < n_ids; k++)
+          if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) {
+            signer = (uint16_t)k;
+            break;
+          }
+      }
+      uint32_t s_off = 0, s_len = 0;
+      bool have = false;
+      {
+        uint32_t pos = mo, end = mo + ml;
+        Fld f;
+#pragma unroll 1
+        while (next_fld(r, pos, end, f) > 0) {
+          if (f.field != 5 || f.wt != 2) continue;
+          Entry se;
+          read_entry(r, f.off, f.len, se);
+          if (key_eq(r, se.koff, se.klen, ge.koff, ge.klen)) {
+            have = true;
+            s_off = se.voff;
+            s_len = se.vlen;
+          }
+        }
+      }
+      uint8_t key = 0xFF;
+      {
+        uint32_t pos = tx_off, end = tx_off + tx_len, j = 0;
+        Fld f;
+#pragma unroll 1
+        while (next_fld(r, pos, end, f) > 0) {
+          if (f.field != 1 || f.wt != 2) continue;
+          uint32_t ko, kl;
+          last_string(r, f.off, f.len, 2, ko, kl);
+          if (key_eq(r, ko, kl, ge.koff, ge.klen)) {
+            key = (uint8_t)j;
+            break;
+          }
+          j++;
+        }
+      }
+      rec(gv.voff, gv.vlen, signer, have && s_len == MOCHI_RSA_BYTES ? s_off : ~0u, key);
+    }
+    return true;
+  });
+}
+
 template <typename Sink>
 __device__ void walk_mg(ByteReader& r, uint32_t mo, uint32_t ml, uint32_t tx_off, uint32_t tx_len,
                         const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids,
@@ -729,15 +783,16 @@ __global__ __launch_bounds__(256) void k_w2_mg(const uint8_t* __restrict__ wire,
     if (!valid_mg_count(r, vo, vl, nge, nse)) {
       bits = kStMal;
     } else if (last == e) {  // this entry's value is the key's final one: it is decoded
-      if (nge > kMaxGrantsPerMG || nse > kMaxSigEntries || !mg_distinct_canonical(r, vo, vl, ng)) bits = kStFb;
-      else if (ng == 1)
-        walk_mg(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids,
-                [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
-                  ce.r_goff[e] = go;
-                  ce.r_glen[e] = gl;
-                  ce.r_sig[e] = so;
-                  ce.r_sk[e] = (uint32_t)sg << 8 | key;
-                });
+      if (nge > kMaxGrantsPerMG || nse > kMaxSigEntries ||
+          !mg_decode_first(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, ng,
+                           [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
+                             // the emit record, read by k_w2_emit_mg when ng == 1
+                             ce.r_goff[e] = go;
+                             ce.r_glen[e] = gl;
+                             ce.r_sig[e] = so;
+                             ce.r_sk[e] = (uint32_t)sg << 8 | key;
+                           }))
+        bits = kStFb;
     }
     ce.last[e] = first ? last : ~0u;
     ce.ng[e] = bits ? 0u : ng;
