@@ -38,6 +38,14 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+bool prep_serial() {
+  static const bool v = [] {
+    const char* e = getenv("MOCHI_PREP_SERIAL");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 uint32_t default_chunk_grants() {
   const char* e = getenv("MOCHI_CHUNK_GRANTS");
   const long x = e ? atol(e) : 0;
@@ -533,7 +541,7 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.op_g0 = o->op_g0;
   a.op_ts = o->op_ts;
   a.op_out_off = op_out_off;
-  a.aux = c->aux;
+  a.aux = prep_serial() ? nullptr : c->aux;  // MOCHI_PREP_SERIAL=1: prep on the launch stream (A/B)
   a.ev_fork = c->ev_fork;
   a.ev_join = c->ev_join;
   if (c->profiling) {
@@ -1256,14 +1264,16 @@ static int decide_fallback(mochi_ctx* c, const mochi_write2_batch* w, const moch
 // ---- Write2 wire path, host memory: chunked pipeline -------------------------
 //
 // Messages are cut into chunks of whole messages (multiples of 32, so each
-// chunk's accept bits start on a word) of ~chunk_grants * 512 wire bytes.  For
-// chunk j: stage + upload (copy-in stream), then on the context stream the
-// decode count phase and its totals; chunk j-1's emit + verify + fix-up is
-// enqueued once ITS totals are on the host, so the host waits only for count
-// kernels while the device verifies the previous chunk and the copy engines
-// move the next one.  Verdicts come down per chunk on the copy-out stream.
+// chunk's accept bits start on a word) of ~chunk_grants * 256 wire bytes.
+// For chunk j:
+// stage + upload (copy-in stream), then on the context stream the decode count
+// phase and its totals; chunk j-2's emit + verify + fix-up is enqueued once ITS
+// totals are on the host, so the host waits only for count kernels while the
+// device verifies earlier chunks and the copy engines move the next one.
+// Verdicts come down per chunk on the copy-out stream.
 static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
                               uint8_t* msg_status, mochi_write2_decoded* dec) {
+  constexpr size_t kW2Lag = 2;  // chunks counted ahead of the one being verified
   int rc;
   const uint32_t M = w->n_msgs;
   for (uint32_t m = 0; m < M; m++)
@@ -1294,7 +1304,11 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     size_t seg[7], cnt;
   };
   std::vector<Chunk> ch;
-  const uint64_t target = dec ? UINT64_MAX : (uint64_t)c->chunk_grants * 512;
+  // ~67 MB of wire bytes per chunk at the default chunk_grants (measured on one
+  // box, 250k messages: 45.5 GB/s at 67 MB, 43.5 at 134 MB, 40.3 at 34 MB; a
+  // ramp of smaller chunks at fill and drain measured 37.7: every chunk pays
+  // the verify path's latency floor, ~0.6 ms, whatever its size)
+  const uint64_t target = dec ? UINT64_MAX : (uint64_t)c->chunk_grants * 256;
   for (uint32_t m0 = 0; m0 < M || ch.empty();) {
     uint32_t m1 = m0;
     uint64_t bytes = 0;
@@ -1456,9 +1470,13 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     if ((rc = w2_count(c, &dw, dout + o_status + k.m0, c->w2_cnt.as<uint32_t>() + k.cnt, tot + 4 * j, c->tot_ev[j], st,
                        &args[j])))
       return rc;
-    if (j > 0 && (rc = finish(j - 1))) return rc;
+    // the verify of chunk j - kW2Lag: its totals are read on the host, so the
+    // host waits for its count; with two chunks of lag the stream still holds
+    // work while it waits
+    if (j >= kW2Lag && (rc = finish(j - kW2Lag))) return rc;
   }
-  if ((rc = finish(nch - 1))) return rc;
+  for (size_t j = nch > kW2Lag ? nch - kW2Lag : 0; j < nch; j++)
+    if ((rc = finish(j))) return rc;
   HIP_TRY(scratch_release(c, st));
   if (dec) {
     // decode-only (one chunk): copy the decoded SoA back (tests / inspection)

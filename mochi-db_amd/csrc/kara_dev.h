@@ -19,10 +19,6 @@
 #include "fold.h"
 #include "mont.h"
 
-#ifndef MOCHI_KARA_FUSE
-#define MOCHI_KARA_FUSE 1
-#endif
-
 namespace mochi {
 
 constexpr int kKH = kL / 2;  // 37: the Karatsuba split
@@ -30,38 +26,20 @@ static_assert(2 * kKH == kL, "even limb count");
 constexpr int kSignedLo = kKH;          // first t limb that may be negative
 constexpr int kSignedHi = 3 * kKH + 1;  // one past the last (t[111] = M_74 + H_37 >= 0, but unnormalised)
 
-// Normalised limbs 0..74 of a 37 x 37 product: emit(k, limb) in order.  SQR:
-// b is a (cross products once, column doubled).  AO / BO: the halves' offsets.
-template <bool SQR, int AO, int BO, int NA, int NB, typename EMIT>
+// Normalised limbs 0..74 of a 37 x 37 product a * b: emit(k, limb) in order.
+// AO / BO: the halves' offsets.
+template <int AO, int BO, int NA, int NB, typename EMIT>
 __device__ __forceinline__ void half_product(const uint32_t (&a)[NA], const uint32_t (&b)[NB], EMIT&& emit) {
   uint64_t carry = 0;
   static_for<0, 2 * kKH - 1>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int lo = k - kKH + 1 > 0 ? k - kKH + 1 : 0;
-    uint64_t acc;
-    if constexpr (SQR) {
-      constexpr int xhi = k > 0 ? (k - 1) / 2 : -1;
-      uint64_t xs = 0;
-      static_for<lo, xhi + 1>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        xs = mad64(a[AO + i], a[AO + k - i], xs);
-      });
-      asm("" : "+v"(xs));  // double the column sum once (else hipcc doubles every a_i)
-      acc = carry + (xs << 1);  // one v_lshl_add_u64
-      if constexpr ((k & 1) == 0) {
-#if MOCHI_KARA_FUSE
-        asm("" : "+v"(acc));  // keep it fused (else hipcc shifts, mads the square, then adds: one op more)
-#endif
-        acc = mad64(a[AO + (k >> 1)], a[AO + (k >> 1)], acc);
-      }
-    } else {
-      constexpr int hi = k < kKH - 1 ? k : kKH - 1;
-      acc = carry;
-      static_for<lo, hi + 1>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        acc = mad64(a[AO + i], b[BO + k - i], acc);
-      });
-    }
+    constexpr int hi = k < kKH - 1 ? k : kKH - 1;
+    uint64_t acc = carry;
+    static_for<lo, hi + 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      acc = mad64(a[AO + i], b[BO + k - i], acc);
+    });
     emit(std::integral_constant<int, k>{}, (uint32_t)acc & kLimbMask);
     carry = acc >> kLimbBits;
     // column by column: left alone the scheduler hoists later columns' mads
@@ -72,27 +50,51 @@ __device__ __forceinline__ void half_product(const uint32_t (&a)[NA], const uint
   emit(std::integral_constant<int, 2 * kKH>{}, (uint32_t)(carry >> kLimbBits));
 }
 
-// t = x * y (SQR: x * x) as 148 limbs: t[0..36] and t[112..147] normalised,
-// t[37..111] signed / unnormalised; t_hi (t[73..147]) leaves with its bytes 0..2
-// XOR kFoldBias (the fold's signed B operand), fused where a limb is final.
-template <bool SQR>
-__device__ __forceinline__ void kara_product(const uint32_t (&x)[kL], const uint32_t (&y)[kL], uint32_t (&t)[2 * kL]) {
-  // M = (x_lo + x_hi)(y_lo + y_hi) -> t[37 + k]
-  {
-    uint32_t sx[kKH];
-#pragma unroll
-    for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
-    if constexpr (SQR) {
-      half_product<true, 0, 0>(sx, sx, [&](auto kc, uint32_t v) { t[kKH + decltype(kc)::value] = v; });
-    } else {
-      uint32_t sy[kKH];
-#pragma unroll
-      for (int i = 0; i < kKH; i++) sy[i] = y[i] + y[kKH + i];
-      half_product<false, 0, 0>(sx, sy, [&](auto kc, uint32_t v) { t[kKH + decltype(kc)::value] = v; });
+// A 37-limb square, product-scanned with the doubling folded into the
+// operands: column k = carry + sum_{i < k-i} (2 a_i) a_{k-i} + a_{k/2}^2, one
+// chain of v_mad_u64_u32 with the square term in it (the schoolbook form sums
+// the cross products, doubles the sum with a v_lshl_add_u64 and needs an asm
+// barrier to keep hipcc from doubling every a_i, whose hazard pads cost ~250
+// s_nop per squaring).  a_m is needed undoubled only up to column 2m (as the
+// higher index of a cross product, or squared) and doubled only after it (as
+// the lower index), so it is doubled IN PLACE right after column 2m: no extra
+// registers, 36 v_lshlrev per square; `a` is clobbered.  hipcc still sums each
+// column's products from zero and adds the carry with one v_lshl_add_u64
+// (re-association).  Bound: limbs of a are < 2^29 (M's a_lo + a_hi), so 2a_i <
+// 2^30, a product < 2^59, and a column < 18 * 2^59 + 2^58 + carry (< 2^36) <
+// 2^64 (tests/fold_model.py asserts every column).
+template <int AO, int NA, typename EMIT>
+__device__ __forceinline__ void half_square(uint32_t (&a)[NA], EMIT&& emit) {
+  uint64_t carry = 0;
+  static_for<0, 2 * kKH - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int lo = k - kKH + 1 > 0 ? k - kKH + 1 : 0;
+    constexpr int xhi = k > 0 ? (k - 1) / 2 : -1;
+    uint64_t acc = carry;
+    static_for<lo, xhi + 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      acc = mad64(a[AO + i], a[AO + k - i], acc);  // a[AO + i] is already 2 a_i
+    });
+    if constexpr ((k & 1) == 0) {
+      acc = mad64(a[AO + (k >> 1)], a[AO + (k >> 1)], acc);
+      if constexpr ((k >> 1) < kKH - 1) a[AO + (k >> 1)] += a[AO + (k >> 1)];
     }
-  }
-  // L = x_lo y_lo: t[k] (+)= L_k, t[37 + k] -= L_k
-  half_product<SQR, 0, 0>(x, y, [&](auto kc, uint32_t v) {
+    emit(std::integral_constant<int, k>{}, (uint32_t)acc & kLimbMask);
+    carry = acc >> kLimbBits;
+    __builtin_amdgcn_sched_barrier(0);  // column by column (see half_product)
+  });
+  emit(std::integral_constant<int, 2 * kKH - 1>{}, (uint32_t)carry & kLimbMask);
+  emit(std::integral_constant<int, 2 * kKH>{}, (uint32_t)(carry >> kLimbBits));
+}
+
+// The combination t = L + 2^(28*37) (M - L - H) + 2^(28*74) H once M is in
+// t[37..111]: L's limbs (run by `low`) and H's (run by `high`) are folded in as
+// their chains emit them -- no limb of L or H is stored.  t_hi (t[73..147])
+// leaves with its bytes 0..2 XOR kFoldBias (the fold's signed B operand),
+// applied where a limb is final.
+template <typename LOW, typename HIGH>
+__device__ __forceinline__ void kara_combine(uint32_t (&t)[2 * kL], LOW&& low, HIGH&& high) {
+  low([&](auto kc, uint32_t v) {  // t[k] (+)= L_k, t[37 + k] -= L_k
     constexpr int k = decltype(kc)::value;
     if constexpr (k < kL) {  // L_74 == 0
       if constexpr (k < kKH) t[k] = v;
@@ -100,9 +102,7 @@ __device__ __forceinline__ void kara_product(const uint32_t (&x)[kL], const uint
       t[kKH + k] -= v;
     }
   });
-  // H = x_hi y_hi: t[37 + m] -= H_m, t[74 + m] (+)= H_m; a t_hi limb is biased
-  // once it is final
-  half_product<SQR, kKH, kKH>(x, y, [&](auto mc, uint32_t v) {
+  high([&](auto mc, uint32_t v) {  // t[37 + m] -= H_m, t[74 + m] (+)= H_m
     constexpr int m = decltype(mc)::value;
     if constexpr (m < kL) {  // H_74 == 0
       t[kKH + m] -= v;
@@ -115,6 +115,34 @@ __device__ __forceinline__ void kara_product(const uint32_t (&x)[kL], const uint
       }
     }
   });
+}
+
+// t = x^2 as 148 limbs (k_rsa_pow): t[0..36] and t[112..147] normalised,
+// t[37..111] signed / unnormalised, t_hi biased.  x is clobbered (the fold
+// overwrites it next).
+__device__ __forceinline__ void kara_square(uint32_t (&x)[kL], uint32_t (&t)[2 * kL]) {
+  {  // M = (x_lo + x_hi)^2 -> t[37 + k]
+    uint32_t sx[kKH];
+#pragma unroll
+    for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
+    half_square<0>(sx, [&](auto kc, uint32_t v) { t[kKH + decltype(kc)::value] = v; });
+  }
+  kara_combine(t, [&](auto&& emit) { half_square<0>(x, emit); }, [&](auto&& emit) { half_square<kKH>(x, emit); });
+}
+
+// t = x * y as 148 limbs (k_rsa_final), the same layout as kara_square.
+__device__ __forceinline__ void kara_product(const uint32_t (&x)[kL], const uint32_t (&y)[kL], uint32_t (&t)[2 * kL]) {
+  {  // M = (x_lo + x_hi)(y_lo + y_hi) -> t[37 + k]
+    uint32_t sx[kKH], sy[kKH];
+#pragma unroll
+    for (int i = 0; i < kKH; i++) {
+      sx[i] = x[i] + x[kKH + i];
+      sy[i] = y[i] + y[kKH + i];
+    }
+    half_product<0, 0>(sx, sy, [&](auto kc, uint32_t v) { t[kKH + decltype(kc)::value] = v; });
+  }
+  kara_combine(t, [&](auto&& emit) { half_product<0, 0>(x, y, emit); },
+               [&](auto&& emit) { half_product<kKH, kKH>(x, y, emit); });
 }
 
 }  // namespace mochi

@@ -72,7 +72,7 @@ __device__ __forceinline__ void final_slot(uint32_t slot, uint32_t base, uint32_
   }
   // ---- t = z * s: one level of Karatsuba (kara_dev.h), t_hi biased ----
   uint32_t t[2 * kL];
-  kara_product<false>(x, sv, t);
+  kara_product(x, sv, t);
   // digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
   uint32_t hl[kHL];
   {

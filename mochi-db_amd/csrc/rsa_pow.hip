@@ -25,13 +25,44 @@
 #include "fold_dev.h"
 #include "rsa_common.h"
 
+// MOCHI_POW_STAMPS (measurement builds only, `make ab`): per wave, s_memtime
+// cycles spent in x^2, in the fold, and in the whole kernel, read back with
+// mochi_debug_pow_stamps() (scripts/pow_stamps.py)
+#ifndef MOCHI_POW_STAMPS
+#define MOCHI_POW_STAMPS 0
+#endif
+
 namespace mochi {
+#if MOCHI_POW_STAMPS
+__device__ unsigned long long g_pow_stamps[4096][4];
+#endif
 namespace {
 
-__device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restrict__ wl, cptr cadd) {
+struct Stamps {
+  uint64_t x2 = 0, fold = 0, n = 0;
+};
+
+__device__ __forceinline__ uint64_t stamp() {
+#if MOCHI_POW_STAMPS
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
+}
+
+__device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restrict__ wl, cptr cadd, Stamps& st) {
   uint32_t t[2 * kL];
-  kara_product<true>(x, x, t);                // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
+  const uint64_t t0 = stamp();
+  kara_square(x, t);  // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
+  const uint64_t t1 = stamp();
   fold_reduce<false, true, true>(t, x, wl, cadd, nullptr);
+  const uint64_t t2 = stamp();
+  st.x2 += t1 - t0;
+  st.fold += t2 - t1;
+  st.n++;
 }
 
 // Persistent: one block per CU walks a contiguous range of 512-slot groups, so
@@ -43,6 +74,8 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const uint32_t* __restrict__
                                                     const uint16_t* __restrict__ signer,
                                                     const FoldKey* __restrict__ fold, uint32_t* __restrict__ zout) {
   __shared__ v4i w[kFoldImgBytes / 16];
+  Stamps st;
+  const uint64_t t_begin = stamp();
   for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
     const uint32_t slot = base + threadIdx.x;
     const uint32_t g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
@@ -59,16 +92,35 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const uint32_t* __restrict__
     for (int it = 0; it < 16; it++) {
       cptr ci = c;
       asm volatile("" : "+s"(ci));  // keep the 74 cadd loads inside the loop (SGPR pressure if hoisted)
-      fold_sqr(x, w + (threadIdx.x & 63), ci);
+      fold_sqr(x, w + (threadIdx.x & 63), ci, st);
     }
     if (active) {
 #pragma unroll
       for (int j = 0; j < kL; j++) zout[(size_t)j * n_slots + slot] = x[j];
     }
   });
+#if MOCHI_POW_STAMPS
+  const uint64_t t_end = stamp();
+  const uint32_t wv = blockIdx.x * 8 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && wv < 4096) {
+    g_pow_stamps[wv][0] = st.x2;
+    g_pow_stamps[wv][1] = st.fold;
+    g_pow_stamps[wv][2] = t_end - t_begin;
+    g_pow_stamps[wv][3] = st.n;
+  }
+#else
+  (void)t_begin;
+#endif
 }
 
 }  // namespace
+
+#if MOCHI_POW_STAMPS
+extern "C" int mochi_debug_pow_stamps(unsigned long long* out, unsigned n_waves) {
+  if (n_waves > 4096) n_waves = 4096;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pow_stamps), 32 * (size_t)n_waves, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t st) {
   const uint32_t blocks = fold_grid(a.n_slots);

@@ -88,9 +88,17 @@ def _columns(a, b, sqr):
     for k in range(2 * na - 1):
         lo, hi = max(0, k - na + 1), min(k, na - 1)
         if sqr:
-            cross = sum(a[i] * a[k - i] for i in range(lo, (k - 1) // 2 + 1) if i < k - i)
-            assert cross < 1 << 64
-            acc = carry + 2 * cross + (a[k // 2] * a[k // 2] if k % 2 == 0 else 0)
+            # kara_dev.h half_square: the lower index of every cross product is
+            # read doubled (a_i is doubled in place after column 2i), the square
+            # term joins the chain; every operand fits 32 bits, every partial
+            # sum 64 bits (the chain only grows, so the final check covers it)
+            acc = carry
+            for i in range(lo, (k - 1) // 2 + 1):
+                if i < k - i:
+                    assert 2 * a[i] < 1 << 32 and a[k - i] < 1 << 32
+                    acc += (2 * a[i]) * a[k - i]
+            if k % 2 == 0:
+                acc += a[k // 2] * a[k // 2]
         else:
             acc = carry + sum(a[i] * b[k - i] for i in range(lo, hi + 1))
         assert acc < 1 << 64, "column sum overflows the 64-bit accumulator"
