@@ -21,29 +21,88 @@ static __constant__ uint32_t kSha256K[64] = {
 
 __device__ __forceinline__ uint32_t sha_rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 
-// Big-endian message word at byte position p (multiple of 4) of the padded message.
-__device__ __forceinline__ uint32_t sha_word(const uint8_t* base, uint32_t p, uint32_t len, uint32_t total) {
-  if (p + 4 <= len) {
-    const uintptr_t addr = (uintptr_t)(base + p);
-    const uint32_t* wp = (const uint32_t*)(addr & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(addr & 3);
-    const uint32_t w0 = wp[0];
-    const uint32_t w1 = sh ? wp[1] : 0u;  // holds message byte p+3 when sh != 0
-    const uint32_t le = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh));
-    return __builtin_bswap32(le);
-  }
-  if (p + 8 == total) return 0;  // high half of the 64-bit bit length (len < 2^29)
-  if (p + 4 == total) return len << 3;
-  uint32_t v = 0;
+// One compression of the 16 big-endian words w into h.
+__device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint32_t i = p + q;
-    uint32_t byte = 0;
-    if (i < len) byte = base[i];
-    else if (i == len) byte = 0x80;
-    v = (v << 8) | byte;
+  for (int t = 0; t < 64; t++) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+      const uint32_t s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
+      wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    const uint32_t S1 = sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
+    const uint32_t S0 = sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + mj;
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
-  return v;
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// The 16 message words of block `blk` of the padded message (FIPS 180-4 5.1.1)
+// of the `len` bytes at `base` (any alignment).  The block's bytes come from
+// 16-byte-aligned dwordx4 loads -- 4 or 5 per block instead of two dword loads
+// and a branch per word -- each issued only if its 16 bytes hold a message
+// byte (so it stays inside the page of a valid byte: the blob may be a slice
+// of a wire buffer), then a per-lane dword rotation (two selects per word,
+// base & 15 is the same for every block), a funnel shift and a byte swap.
+// Words at or past the end take the padding: data bytes, 0x80, zeros, and
+// the 64-bit bit length (len < 2^29) in the last two words of the last block.
+__device__ __forceinline__ void sha256_block_words(const uint8_t* base, uint32_t len, uint32_t blk, uint32_t total,
+                                                   uint32_t (&w)[16]) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const uintptr_t addr = (uintptr_t)base + 64u * blk;
+  const v4u* a16 = (const v4u*)(addr & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(addr & 15);
+  const int64_t p0 = (int64_t)(64u * blk) - sh;  // message position of the first loaded byte
+  uint32_t d[20];
+#pragma unroll
+  for (int c = 0; c < 5; c++) {
+    v4u v = {0u, 0u, 0u, 0u};
+    if (len != 0 && p0 + 16 * c < (int64_t)len && (c < 4 || sh != 0)) v = a16[c];
+    d[4 * c] = v.x;
+    d[4 * c + 1] = v.y;
+    d[4 * c + 2] = v.z;
+    d[4 * c + 3] = v.w;
+  }
+  // e[j] = d[j + (sh >> 2)], j = 0..16, as two rounds of mask selects (a
+  // ternary here is turned into a dynamically indexed array in scratch)
+  const uint32_t m4 = 0u - ((sh >> 2) & 1u), m8 = 0u - ((sh >> 3) & 1u);
+  uint32_t e1[19], e[17];
+#pragma unroll
+  for (int j = 0; j < 19; j++) e1[j] = (d[j + 1] & m4) | (d[j] & ~m4);
+#pragma unroll
+  for (int j = 0; j < 17; j++) e[j] = (e1[j + 2] & m8) | (e1[j] & ~m8);
+  const uint32_t r = 8 * (sh & 3);
+  // every lane's block is all message bytes (the common case): no padding work
+  const bool full = __ballot(64u * blk + 64 > len) == 0;
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    const uint32_t le = __builtin_amdgcn_alignbit(e[t + 1], e[t], r);
+    uint32_t v = __builtin_bswap32(le);
+    if (!full) {
+      const uint32_t p = 64u * blk + 4u * t;
+      if (p + 8 == total) {
+        v = 0;  // high half of the bit length
+      } else if (p + 4 == total) {
+        v = len << 3;
+      } else if (p + 4 > len) {
+        // n data bytes (0..3), then 0x80 if the message ends inside this word
+        const uint32_t n = p < len ? len - p : 0;
+        const uint32_t keep = n ? ~0u << (32 - 8 * n) : 0u;
+        v = (v & keep) | (p + n == len ? 0x80u << (24 - 8 * n) : 0u);
+      }
+    }
+    w[t] = v;
+  }
 }
 
 __device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8]) {
@@ -54,30 +113,8 @@ __device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8
 #pragma unroll 1
   for (uint32_t blk = 0; blk < nblocks; blk++) {
     uint32_t w[16];
-#pragma unroll
-    for (int t = 0; t < 16; t++) w[t] = sha_word(base, blk * 64 + 4 * t, len, total);
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll
-    for (int t = 0; t < 64; t++) {
-      uint32_t wt;
-      if (t < 16) {
-        wt = w[t];
-      } else {
-        const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-        const uint32_t s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
-        const uint32_t s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
-        wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-        w[t & 15] = wt;
-      }
-      const uint32_t S1 = sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25);
-      const uint32_t ch = (e & f) ^ (~e & g);
-      const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
-      const uint32_t S0 = sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22);
-      const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-      const uint32_t t2 = S0 + mj;
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-    }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+    sha256_block_words(base, len, blk, total, w);
+    sha256_compress(h, w);
   }
 }
 
