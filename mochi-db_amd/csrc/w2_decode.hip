@@ -176,18 +176,39 @@ __device__ bool valid_grant_at(ByteReader& r, uint32_t off, uint32_t len) {
   return parse_grant(g, ts, ho, hl);
 }
 
-// map<string, V> entry; kind 0 = bytes value, 1 = Grant value
-__device__ bool valid_leaf_entry(ByteReader& r, uint32_t off, uint32_t len, int kind) {
+struct Entry {
+  uint32_t koff, klen;  // key (last occurrence; default "")
+  uint32_t voff, vlen;  // value (last occurrence; default empty)
+  uint32_t nval;
+};
+
+// map<string, V> entry; kind 0 = bytes value, 1 = Grant value: validated, and
+// its key and value read as read_entry reads them (last occurrence of each)
+__device__ bool valid_leaf_read(ByteReader& r, uint32_t off, uint32_t len, int kind, Entry& e) {
+  e.koff = e.klen = e.voff = e.vlen = e.nval = 0;
   uint32_t pos = off, end = off + len;
   Fld f;
   int rc;
 #pragma unroll 1
   while ((rc = next_fld(r, pos, end, f)) > 0) {
     if (f.wt != 2) continue;
-    if (f.field == 1 && !valid_utf8(r, f.off, f.len)) return false;
-    if (f.field == 2 && kind == 1 && !valid_grant_at(r, f.off, f.len)) return false;
+    if (f.field == 1) {
+      if (!valid_utf8(r, f.off, f.len)) return false;
+      e.koff = f.off;
+      e.klen = f.len;
+    } else if (f.field == 2) {
+      if (kind == 1 && !valid_grant_at(r, f.off, f.len)) return false;
+      e.voff = f.off;
+      e.vlen = f.len;
+      e.nval++;
+    }
   }
   return rc == 0;
+}
+
+__device__ __forceinline__ bool valid_leaf_entry(ByteReader& r, uint32_t off, uint32_t len, int kind) {
+  Entry e;
+  return valid_leaf_read(r, off, len, kind, e);
 }
 
 __device__ bool valid_multigrant(ByteReader& r, uint32_t off, uint32_t len) {
@@ -257,11 +278,6 @@ __device__ bool valid_write2(ByteReader& r) {
 }
 
 // ---- extraction on a valid message -------------------------------------------
-struct Entry {
-  uint32_t koff, klen;  // key (last occurrence; default "")
-  uint32_t voff, vlen;  // value (last occurrence; default empty)
-  uint32_t nval;
-};
 
 __device__ void read_entry(ByteReader& r, uint32_t off, uint32_t len, Entry& e) {
   e.koff = e.klen = e.voff = e.vlen = e.nval = 0;
@@ -536,28 +552,67 @@ __device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint
   return rc < 0 ? kStMal : 0u;
 }
 
-// Validate a MultiGrant value (valid_multigrant) and count its grants /
-// grantSignatures entries on the wire.
-__device__ bool valid_mg_count(ByteReader& r, uint32_t off, uint32_t len, uint32_t& nge,
-                                            uint32_t& nse) {
+// One walk of a MultiGrant value: validates it as valid_multigrant does,
+// counts its grants / grantSignatures entries on the wire, and records what
+// the decode of the common shape needs -- the last entry of each map (its key
+// and value as read_entry reads them) and the last serverId -- so that shape
+// (one grants entry, at most one signature entry) is decoded without walking
+// the value again.
+struct MGScan {
+  uint32_t nge, nse;
+  Entry g, sg;               // last grants / grantSignatures entry
+  uint32_t sid_off, sid_len;  // MultiGrant.serverId (last)
+};
+
+__device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan& m) {
   uint32_t pos = off, end = off + len;
   Fld f;
   int rc;
-  nge = nse = 0;
+  m.nge = m.nse = 0;
+  m.sid_off = m.sid_len = 0;
 #pragma unroll 1
   while ((rc = next_fld(r, pos, end, f)) > 0) {
     if (f.wt != 2) continue;
     if (f.field == 1) {
-      nge++;
-      if (!valid_leaf_entry(r, f.off, f.len, 1)) return false;
+      m.nge++;
+      if (!valid_leaf_read(r, f.off, f.len, 1, m.g)) return false;
     } else if (f.field >= 2 && f.field <= 4) {
       if (!valid_utf8(r, f.off, f.len)) return false;
+      if (f.field == 4) {
+        m.sid_off = f.off;
+        m.sid_len = f.len;
+      }
     } else if (f.field == 5) {
-      nse++;
-      if (!valid_leaf_entry(r, f.off, f.len, 0)) return false;
+      m.nse++;
+      if (!valid_leaf_read(r, f.off, f.len, 0, m.sg)) return false;
     }
   }
   return rc == 0;
+}
+
+// signer = index of the key whose server id is the MultiGrant's serverId
+__device__ __forceinline__ uint16_t find_signer(ByteReader& r, uint32_t so, uint32_t sl, const uint8_t* __restrict__ ids,
+                                                const uint32_t* __restrict__ id_off, uint32_t n_ids) {
+#pragma unroll 1
+  for (uint32_t k = 0; k < n_ids; k++)
+    if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) return (uint16_t)k;
+  return 0xFFFF;
+}
+
+// key slot = index of the first op of the transaction naming `key`
+__device__ __forceinline__ uint8_t find_key_slot(ByteReader& r, uint32_t tx_off, uint32_t tx_len, uint32_t ko,
+                                                 uint32_t kl) {
+  uint32_t pos = tx_off, end = tx_off + tx_len, j = 0;
+  Fld f;
+#pragma unroll 1
+  while (next_fld(r, pos, end, f) > 0) {
+    if (f.field != 1 || f.wt != 2) continue;
+    uint32_t oo, ol;
+    last_string(r, f.off, f.len, 2, oo, ol);
+    if (key_eq(r, oo, ol, ko, kl)) return (uint8_t)j;
+    j++;
+  }
+  return 0xFF;
 }
 
 // Certificate entries (compact, in wire order per message): message index,
@@ -594,16 +649,11 @@ __device__ bool mg_decode_first(ByteReader& r, uint32_t mo, uint32_t ml, uint32_
   return for_map(r, mo, ml, 1, [&](const Entry& ge, const Entry& gv) -> bool {
     if (!grant_canonical(r, gv.voff, gv.vlen)) return false;
     if (ng++ == 0) {
-      uint16_t signer = 0xFFFF;
+      uint16_t signer;
       {
         uint32_t so, sl;
         last_string(r, mo, ml, 4, so, sl);  // MultiGrant.serverId
-#pragma unroll 1
-        for (uint32_t k = 0; k < n_ids; k++)
-          if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) {
-            signer = (uint16_t)k;
-            break;
-          }
+        signer = find_signer(r, so, sl, ids, id_off, n_ids);
       }
       uint32_t s_off = 0, s_len = 0;
       bool have = false;
@@ -622,22 +672,7 @@ __device__ bool mg_decode_first(ByteReader& r, uint32_t mo, uint32_t ml, uint32_
           }
         }
       }
-      uint8_t key = 0xFF;
-      {
-        uint32_t pos = tx_off, end = tx_off + tx_len, j = 0;
-        Fld f;
-#pragma unroll 1
-        while (next_fld(r, pos, end, f) > 0) {
-          if (f.field != 1 || f.wt != 2) continue;
-          uint32_t ko, kl;
-          last_string(r, f.off, f.len, 2, ko, kl);
-          if (key_eq(r, ko, kl, ge.koff, ge.klen)) {
-            key = (uint8_t)j;
-            break;
-          }
-          j++;
-        }
-      }
+      const uint8_t key = find_key_slot(r, tx_off, tx_len, ge.koff, ge.klen);
       rec(gv.voff, gv.vlen, signer, have && s_len == MOCHI_RSA_BYTES ? s_off : ~0u, key);
     }
     return true;
@@ -712,7 +747,9 @@ __device__ __forceinline__ void emit_grant(const W2Out& out, uint32_t g, uint64_
 
 // Level 1.  cnt_o[m] = operations on the wire (k_w2_final turns it into the
 // decoded count).  Element M of cnt_ce is the scan's extra element.
-__global__ __launch_bounds__(256) void k_w2_msg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+// three waves per SIMD (the register cap keeps the level-1 walk at the occupancy
+// it had before the level-2 scan shared its leaf walker)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_w2_msg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
                                                 const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m > M) return;
@@ -759,10 +796,11 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
 }
 
 // Level 2 (lane = certificate entry; grid-stride over the device-side total).
-__global__ __launch_bounds__(256) void k_w2_mg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
-                                               const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce,
-                                               const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off,
-                                               uint32_t n_ids) {
+// (capping registers for 4 or 5 waves per SIMD measured 1.4 % and 35 % slower:
+// the walk is instruction-bound, not latency-bound)
+__global__ __launch_bounds__(256) void k_w2_mg(
+    const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff, const uint32_t* __restrict__ mlen, uint32_t M,
+    W2Msg s, CE ce, const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids) {
   const uint32_t total = s.ce_base[M];
 #pragma unroll 1
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -779,20 +817,35 @@ __global__ __launch_bounds__(256) void k_w2_mg(const uint8_t* __restrict__ wire,
         else last = j;
       }
     const uint32_t vo = ce.voff[e], vl = ce.vlen[e];
-    uint32_t bits = 0, ng = 0, nge, nse;
-    if (!valid_mg_count(r, vo, vl, nge, nse)) {
+    uint32_t bits = 0, ng = 0;
+    MGScan sc;
+    // the emit record, read by k_w2_emit_mg when ng == 1
+    auto rec = [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
+      ce.r_goff[e] = go;
+      ce.r_glen[e] = gl;
+      ce.r_sig[e] = so;
+      ce.r_sk[e] = (uint32_t)sg << 8 | key;
+    };
+    if (!valid_mg_scan(r, vo, vl, sc)) {
       bits = kStMal;
     } else if (last == e) {  // this entry's value is the key's final one: it is decoded
-      if (nge > kMaxGrantsPerMG || nse > kMaxSigEntries ||
-          !mg_decode_first(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, ng,
-                           [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
-                             // the emit record, read by k_w2_emit_mg when ng == 1
-                             ce.r_goff[e] = go;
-                             ce.r_glen[e] = gl;
-                             ce.r_sig[e] = so;
-                             ce.r_sk[e] = (uint32_t)sg << 8 | key;
-                           }))
+      if (sc.nge == 1 && sc.nse <= 1) {
+        // the common shape, from the scan: the one grants entry is its key's
+        // first and last; its signature is the signature entry if that entry's
+        // key is the grant's (walk_mg's lookup over one entry)
+        if (sc.g.nval > 1 || !grant_canonical(r, sc.g.voff, sc.g.vlen)) {
+          bits = kStFb;
+        } else {
+          ng = 1;
+          const bool have = sc.nse == 1 && key_eq(r, sc.sg.koff, sc.sg.klen, sc.g.koff, sc.g.klen);
+          rec(sc.g.voff, sc.g.vlen, find_signer(r, sc.sid_off, sc.sid_len, ids, id_off, n_ids),
+              have && sc.sg.vlen == MOCHI_RSA_BYTES ? sc.sg.voff : ~0u,
+              find_key_slot(r, s.tx_off[m], s.tx_len[m], sc.g.koff, sc.g.klen));
+        }
+      } else if (sc.nge > kMaxGrantsPerMG || sc.nse > kMaxSigEntries ||
+                 !mg_decode_first(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, ng, rec)) {
         bits = kStFb;
+      }
     }
     ce.last[e] = first ? last : ~0u;
     ce.ng[e] = bits ? 0u : ng;
