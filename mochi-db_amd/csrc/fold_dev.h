@@ -78,19 +78,18 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
   });
   // ---- x = t_lo + fold(t_hi) + cadd (- h), M-tile by M-tile, carries low to high ----
   int64_t carry = 0;
-  static_for<0, kFoldMT>([&](auto mc) {
+  // one M-tile: 10 K-steps x 2 N-tiles, the next A fragment read one step ahead
+  auto mfma_step = [&](auto mc, auto sc, v16i& d0, v16i& d1) {
+    constexpr int mt = decltype(mc)::value, s = decltype(sc)::value;
+    v4i an = a;
+    if constexpr (mt * kFoldKS + s + 1 < kFoldMT * kFoldKS) an = wl[(mt * kFoldKS + s + 1) * 64];
+    d0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0, 0, 0, 0);
+    d1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1, 0, 0, 0);
+    a = an;
+  };
+  // the limbs of M-tile mt from its accumulators
+  auto assemble = [&](auto mc, const v16i& d0, const v16i& d1) {
     constexpr int mt = decltype(mc)::value;
-    __builtin_amdgcn_sched_barrier(0);
-    v16i d0 = {}, d1 = {};
-    static_for<0, kFoldKS>([&](auto sc) {  // one K-step of weights in flight
-      constexpr int s = decltype(sc)::value;
-      v4i an = a;
-      if constexpr (mt * kFoldKS + s + 1 < kFoldMT * kFoldKS) an = wl[(mt * kFoldKS + s + 1) * 64];
-      d0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0, 0, 0, 0);
-      d1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      a = an;
-    });
     // the two halves of each limb (c0 + 2^8 c1 and c2 + 2^8 c3) in the MFMA's
     // own layout -- half h of the wave holds limb 2u + h of both N-tiles'
     // signatures, all four digits in one lane (rows 4h + 8u + 0..3) -- then one
@@ -127,6 +126,15 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
         carry = v >> kLimbBits;
       }
     });
+  };
+  static_for<0, kFoldMT>([&](auto mc) {
+    __builtin_amdgcn_sched_barrier(0);
+    v16i d0 = {}, d1 = {};
+    static_for<0, kFoldKS>([&](auto sc) {  // one K-step of weights in flight
+      mfma_step(mc, sc, d0, d1);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    assemble(mc, d0, d1);
   });
 }
 
