@@ -319,8 +319,13 @@ __device__ bool bytes_eq(const uint8_t* A, uint32_t a, const uint8_t* B, uint32_
   return true;
 }
 
+// Keys of one map mostly share a prefix ("server-" + UUID, "key-" + number):
+// compare the last four bytes first, so a mismatch costs one word per side.
 __device__ __forceinline__ bool key_eq(ByteReader& r, uint32_t a, uint32_t al, uint32_t b, uint32_t bl) {
-  return al == bl && (a == b || bytes_eq(r.base, a, r.base, b, al));
+  if (al != bl) return false;
+  if (a == b) return true;
+  if (al >= 4 && ld4(r.base, a + al - 4) != ld4(r.base, b + al - 4)) return false;
+  return bytes_eq(r.base, a, r.base, b, al);
 }
 
 // Walk the map entries (field `field`, wt 2) of [off, off+len) in wire order.
@@ -590,12 +595,73 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
   return rc == 0;
 }
 
-// signer = index of the key whose server id is the MultiGrant's serverId
+// signer = index of the key whose server id is the MultiGrant's serverId.
+// The ids share their prefix ("server-"): the last word filters the
+// candidates (its table-side load is the same address in every lane), and
+// only a candidate is compared in full.
+// `tab` (optional): the server ids staged in LDS by the block -- lengths, last
+// words and the bytes themselves at word-aligned offsets -- so the lookup
+// reads the MultiGrant's serverId once (independent word loads) and compares
+// it with LDS words (the same address in every lane: a broadcast) instead of
+// a byte-compare loop of dependent global loads per candidate.
+constexpr uint32_t kIdTab = 64, kIdTabWords = 1024, kIdFast = 16;  // ids, LDS words, words compared from registers
+struct IdTab {
+  uint32_t len[kIdTab], tail[kIdTab], pos[kIdTab];  // pos: first LDS word, ~0 = not staged
+  uint32_t w[kIdTabWords];
+};
+
+__device__ __forceinline__ void stage_ids(IdTab& tab, const uint8_t* __restrict__ ids,
+                                          const uint32_t* __restrict__ id_off, uint32_t n_ids) {
+  if (threadIdx.x == 0) {  // word positions (tiny: a handful of ids)
+    uint32_t p = 0;
+    for (uint32_t k = 0; k < n_ids && k < kIdTab; k++) {
+      const uint32_t l = id_off[k + 1] - id_off[k], nw = (l + 3) / 4;
+      tab.len[k] = l;
+      tab.pos[k] = p + nw <= kIdTabWords ? p : ~0u;
+      if (p + nw <= kIdTabWords) p += nw;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < n_ids && k < kIdTab; k += blockDim.x) {
+    const uint32_t o = id_off[k], l = tab.len[k];
+    tab.tail[k] = l >= 4 ? ld4(ids, o + l - 4) : 0u;
+    if (tab.pos[k] != ~0u)
+      for (uint32_t t = 0; 4 * t < l; t++) {
+        uint32_t v = 0;
+        for (uint32_t j = 0; j < 4 && 4 * t + j < l; j++) v |= (uint32_t)ids[o + 4 * t + j] << (8 * j);
+        tab.w[tab.pos[k] + t] = v;
+      }
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ uint16_t find_signer(ByteReader& r, uint32_t so, uint32_t sl, const uint8_t* __restrict__ ids,
-                                                const uint32_t* __restrict__ id_off, uint32_t n_ids) {
+                                                const uint32_t* __restrict__ id_off, uint32_t n_ids,
+                                                const IdTab* tab = nullptr) {
+  const uint32_t tail = sl >= 4 ? ld4(r.base, so + sl - 4) : 0u;
+  const bool fast = tab && sl >= 4 && sl <= 4 * kIdFast;
 #pragma unroll 1
-  for (uint32_t k = 0; k < n_ids; k++)
-    if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) return (uint16_t)k;
+  for (uint32_t k = 0; k < n_ids; k++) {
+    if (tab && k < kIdTab) {
+      if (tab->len[k] != sl || (sl >= 4 && tab->tail[k] != tail)) continue;
+      if (fast && tab->pos[k] != ~0u) {
+        // a candidate (usually the only one): its whole words against the
+        // serverId's, loads independent of each other (no early exit), then
+        // the last four bytes, already equal (the filter)
+        uint32_t diff = 0;
+        const uint32_t* w = tab->w + tab->pos[k];
+#pragma unroll
+        for (uint32_t t = 0; t < kIdFast; t++)
+          if (4 * t + 4 <= sl) diff |= ld4(r.base, so + 4 * t) ^ w[t];
+        if (diff == 0) return (uint16_t)k;
+        continue;
+      }
+    } else {
+      if (id_off[k + 1] - id_off[k] != sl) continue;
+      if (sl >= 4 && ld4(ids, id_off[k] + sl - 4) != tail) continue;
+    }
+    if (bytes_eq(ids, id_off[k], r.base, so, sl)) return (uint16_t)k;
+  }
   return 0xFFFF;
 }
 
@@ -683,16 +749,11 @@ template <typename Sink>
 __device__ void walk_mg(ByteReader& r, uint32_t mo, uint32_t ml, uint32_t tx_off, uint32_t tx_len,
                         const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids,
                         Sink&& sink) {
-  uint16_t signer = 0xFFFF;
+  uint16_t signer;
   {
     uint32_t so, sl;
     last_string(r, mo, ml, 4, so, sl);  // MultiGrant.serverId
-#pragma unroll 1
-    for (uint32_t k = 0; k < n_ids; k++)
-      if (id_off[k + 1] - id_off[k] == sl && bytes_eq(ids, id_off[k], r.base, so, sl)) {
-        signer = (uint16_t)k;
-        break;
-      }
+    signer = find_signer(r, so, sl, ids, id_off, n_ids);
   }
   for_map(r, mo, ml, 1, [&](const Entry& ge, const Entry& gv) -> bool {
     // grantSignatures[key]: the last entry with this key, its (last) value
@@ -796,14 +857,51 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
 }
 
 // Level 2 (lane = certificate entry; grid-stride over the device-side total).
+// MOCHI_W2_STAMPS (measurement builds only, `make ab VSRC=w2_decode`): per
+// wave, s_memtime ticks spent between the marks of k_w2_mg (dedup, scan,
+// canonical check, signer, key slot, records), read back with
+// mochi_debug_w2_stamps() (scripts/w2_stamps.py)
+#ifndef MOCHI_W2_STAMPS
+#define MOCHI_W2_STAMPS 0
+#endif
+#if MOCHI_W2_STAMPS
+__device__ unsigned long long g_w2_stamps[16384][8];
+#endif
+struct W2Stamps {
+#if MOCHI_W2_STAMPS
+  uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0}, last = 0;
+  __device__ __forceinline__ void mark(int i) {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    if (i) acc[i] += t - last;
+    last = t;
+  }
+  __device__ __forceinline__ void store() {
+    const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0 && w < 16384) {
+      for (int i = 1; i < 7; i++) g_w2_stamps[w][i] = acc[i];
+      g_w2_stamps[w][7] = 1;
+    }
+  }
+#else
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void store() {}
+#endif
+};
+
 // (capping registers for 4 or 5 waves per SIMD measured 1.4 % and 35 % slower:
 // the walk is instruction-bound, not latency-bound)
 __global__ __launch_bounds__(256) void k_w2_mg(
     const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff, const uint32_t* __restrict__ mlen, uint32_t M,
     W2Msg s, CE ce, const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids) {
+  __shared__ IdTab tab;
+  stage_ids(tab, ids, id_off, n_ids);
   const uint32_t total = s.ce_base[M];
+  W2Stamps stp;
 #pragma unroll 1
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    stp.mark(0);
     const uint32_t m = ce.msg[e];
     ByteReader r;
     r.init(wire + moff[m], mlen[m]);
@@ -826,21 +924,28 @@ __global__ __launch_bounds__(256) void k_w2_mg(
       ce.r_sig[e] = so;
       ce.r_sk[e] = (uint32_t)sg << 8 | key;
     };
-    if (!valid_mg_scan(r, vo, vl, sc)) {
+    stp.mark(1);
+    const bool valid = valid_mg_scan(r, vo, vl, sc);
+    stp.mark(2);
+    if (!valid) {
       bits = kStMal;
     } else if (last == e) {  // this entry's value is the key's final one: it is decoded
       if (sc.nge == 1 && sc.nse <= 1) {
         // the common shape, from the scan: the one grants entry is its key's
         // first and last; its signature is the signature entry if that entry's
         // key is the grant's (walk_mg's lookup over one entry)
-        if (sc.g.nval > 1 || !grant_canonical(r, sc.g.voff, sc.g.vlen)) {
+        const bool canon = sc.g.nval <= 1 && grant_canonical(r, sc.g.voff, sc.g.vlen);
+        stp.mark(3);
+        if (!canon) {
           bits = kStFb;
         } else {
           ng = 1;
           const bool have = sc.nse == 1 && key_eq(r, sc.sg.koff, sc.sg.klen, sc.g.koff, sc.g.klen);
-          rec(sc.g.voff, sc.g.vlen, find_signer(r, sc.sid_off, sc.sid_len, ids, id_off, n_ids),
-              have && sc.sg.vlen == MOCHI_RSA_BYTES ? sc.sg.voff : ~0u,
-              find_key_slot(r, s.tx_off[m], s.tx_len[m], sc.g.koff, sc.g.klen));
+          const uint16_t signer = find_signer(r, sc.sid_off, sc.sid_len, ids, id_off, n_ids, &tab);
+          stp.mark(4);
+          const uint8_t slot = find_key_slot(r, s.tx_off[m], s.tx_len[m], sc.g.koff, sc.g.klen);
+          stp.mark(5);
+          rec(sc.g.voff, sc.g.vlen, signer, have && sc.sg.vlen == MOCHI_RSA_BYTES ? sc.sg.voff : ~0u, slot);
         }
       } else if (sc.nge > kMaxGrantsPerMG || sc.nse > kMaxSigEntries ||
                  !mg_decode_first(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, ng, rec)) {
@@ -850,7 +955,9 @@ __global__ __launch_bounds__(256) void k_w2_mg(
     ce.last[e] = first ? last : ~0u;
     ce.ng[e] = bits ? 0u : ng;
     if (bits) atomicOr(s.st_bits + m, bits);
+    stp.mark(6);
   }
+  stp.store();
 }
 
 // Per message: final status and the decoded counts.
@@ -990,14 +1097,25 @@ __global__ __launch_bounds__(256) void k_w2_sig(const uint8_t* __restrict__ wire
   const uint64_t src = sig_src[g];
   uint4 v = make_uint4(0, 0, 0, 0);
   if (src != ~0ull) {
-    const uint8_t* p = wire + src + 16 * q;
-    const uintptr_t a = (uintptr_t)p;
-    if ((a & 3) == 0) {
-      const uint32_t* w = (const uint32_t*)p;
-      v = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-      v = make_uint4(ld4(p, 0), ld4(p, 4), ld4(p, 8), ld4(p, 12));
-    }
+    // the lane's 16 bytes from the one or two 16-byte-aligned chunks holding
+    // them (each chunk holds a signature byte: page-safe), shifted by a dword
+    // rotation (mask selects) and a funnel shift -- two dwordx4 loads instead
+    // of eight dword loads
+    const uintptr_t a = (uintptr_t)(wire + src) + 16 * q;
+    const uint4* c = (const uint4*)(a & ~(uintptr_t)15);
+    const uint32_t sh = (uint32_t)(a & 15);
+    const uint4 c0 = c[0];
+    const uint4 c1 = sh ? c[1] : make_uint4(0, 0, 0, 0);
+    const uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const uint32_t m4 = 0u - ((sh >> 2) & 1u), m8 = 0u - ((sh >> 3) & 1u);
+    uint32_t e1[7], e[5];
+#pragma unroll
+    for (int j = 0; j < 7; j++) e1[j] = (d[j + 1] & m4) | (d[j] & ~m4);
+#pragma unroll
+    for (int j = 0; j < 5; j++) e[j] = (e1[j + 2] & m8) | (e1[j] & ~m8);
+    const uint32_t r = 8 * (sh & 3);
+    v = make_uint4(__builtin_amdgcn_alignbit(e[1], e[0], r), __builtin_amdgcn_alignbit(e[2], e[1], r),
+                   __builtin_amdgcn_alignbit(e[3], e[2], r), __builtin_amdgcn_alignbit(e[4], e[3], r));
   }
   ((uint4*)(sig + (size_t)g * MOCHI_RSA_BYTES))[q] = v;
 }
@@ -1099,3 +1217,13 @@ hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reas
 }
 
 }  // namespace mochi
+
+#if MOCHI_W2_STAMPS
+extern "C" int mochi_debug_w2_stamps(unsigned long long* out, unsigned n_waves) {
+  if (n_waves > 16384) n_waves = 16384;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mochi::g_w2_stamps), 64 * (size_t)n_waves, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif
