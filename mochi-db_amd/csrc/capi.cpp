@@ -877,6 +877,7 @@ int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_
   a->cnt_ce = cnt + 6 * m1;
   a->ce = cnt + (size_t)mochi::kW2MsgArrays * m1;
   a->ce_cap = mochi::kW2MaxCertEntries * (uint32_t)m1;
+  a->inl = (uint32_t*)(((uintptr_t)(a->ce + 11 * (size_t)a->ce_cap) + 15) & ~(uintptr_t)15);
   a->status = status;
   a->scan_temp = c->w2_scan.p;
   a->scan_temp_bytes = c->w2_scan.cap;

@@ -30,6 +30,7 @@ struct W2Args {
   uint32_t* cnt_ce;
   uint32_t* ce;
   uint32_t ce_cap;
+  uint32_t* inl;  // [M+1][kW2InlEntries][4], 16-byte aligned: level 1's first entries (key / value slices)
   uint8_t* status;  // [M]
   void* scan_temp;
   size_t scan_temp_bytes;
@@ -55,8 +56,12 @@ struct W2Args {
 // kW2MaxCertEntries per message on the fast path, 11 words each).
 constexpr uint32_t kW2MaxCertEntries = 32;
 constexpr int kW2MsgArrays = 13;
+// Level 1 records the key / value slices of a message's first kW2InlEntries
+// certificate entries, so the compact entry list is copied, not re-parsed.
+constexpr uint32_t kW2InlEntries = 4;
 inline size_t w2_scratch_words(uint32_t M) {
-  return (size_t)kW2MsgArrays * ((size_t)M + 1) + 11 * (size_t)kW2MaxCertEntries * ((size_t)M + 1);
+  return (size_t)kW2MsgArrays * ((size_t)M + 1) + 11 * (size_t)kW2MaxCertEntries * ((size_t)M + 1) +
+         4 * (size_t)kW2InlEntries * ((size_t)M + 1) + 4;  // + 4: the records start 16-byte aligned
 }
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
 hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans

@@ -455,6 +455,7 @@ struct W2Out {
 // Per-message decode state (W2Args::cnt_ce onwards; cnt_o is W2Args::cnt_o).
 struct W2Msg {
   uint32_t *cnt_ce, *ce_base, *st_bits, *wc_off, *wc_len, *tx_off, *tx_len, *cnt_o;
+  uint32_t* inl;  // [M][kW2InlEntries][4]: koff, klen, voff, vlen of the first entries
 };
 
 // ---- level by level ------------------------------------------------------------
@@ -485,7 +486,7 @@ __device__ __noinline__ bool valid_write2_whole(const uint8_t* base, uint32_t le
 // Level 1 for one message; returns status bits.  nce = certificate entries,
 // nops = operations (both 0 when the message left the fast path).
 __device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint32_t& wc_off, uint32_t& wc_len,
-                              uint32_t& tx_off, uint32_t& tx_len) {
+                              uint32_t& tx_off, uint32_t& tx_len, uint32_t* __restrict__ inl) {
   uint32_t n_wc = 0, n_tx = 0;
   bool whole = false;
   nce = nops = 0;
@@ -513,15 +514,25 @@ __device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint
           break;
         }
         uint32_t p3 = g.off, e3 = g.off + g.len, nval = 0;
+        uint32_t ko = 0, kl = 0, vo = 0, vl = 0;  // read_entry's slices (last key, last value)
         Fld h;
         int rc3;
 #pragma unroll 1
         while ((rc3 = next_fld(r, p3, e3, h)) > 0) {
           if (h.wt != 2) continue;
-          if (h.field == 1 && !valid_utf8(r, h.off, h.len)) return kStMal;
-          if (h.field == 2) nval++;
+          if (h.field == 1) {
+            if (!valid_utf8(r, h.off, h.len)) return kStMal;
+            ko = h.off;
+            kl = h.len;
+          }
+          if (h.field == 2) {
+            nval++;
+            vo = h.off;
+            vl = h.len;
+          }
         }
         if (rc3 < 0) return kStMal;
+        if (nce <= kW2InlEntries) ((uint4*)inl)[nce - 1] = make_uint4(ko, kl, vo, vl);
         if (nval > 1) {
           whole = true;
           break;
@@ -821,7 +832,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
   uint32_t nce, nops, wo = 0, wl = 0, to = 0, tl = 0;
-  const uint32_t bits = msg_level(r, nce, nops, wo, wl, to, tl);
+  const uint32_t bits = msg_level(r, nce, nops, wo, wl, to, tl, s.inl + (size_t)4 * kW2InlEntries * m);
   if (bits) nce = nops = 0;
   s.cnt_ce[m] = nce;
   s.cnt_o[m] = nops;
@@ -836,10 +847,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
                                                     const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M || s.cnt_ce[m] == 0) return;
+  if (m >= M) return;
+  const uint32_t nce = s.cnt_ce[m];
+  if (nce == 0) return;
+  uint32_t e = s.ce_base[m];
+  if (nce <= kW2InlEntries) {  // recorded by level 1: copy
+    const uint4* q = (const uint4*)(s.inl + (size_t)4 * kW2InlEntries * m);
+#pragma unroll 1
+    for (uint32_t j = 0; j < nce; j++, e++) {
+      const uint4 v = q[j];
+      ce.msg[e] = m;
+      ce.koff[e] = v.x;
+      ce.klen[e] = v.y;
+      ce.voff[e] = v.z;
+      ce.vlen[e] = v.w;
+    }
+    return;
+  }
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
-  uint32_t e = s.ce_base[m], pos = s.wc_off[m];
+  uint32_t pos = s.wc_off[m];
   const uint32_t end = pos + s.wc_len[m];
   Fld f;
 #pragma unroll 1
@@ -1151,7 +1178,7 @@ inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b
 W2Msg msg_view(const W2Args& a) {
   const size_t m1 = (size_t)a.M + 1;
   uint32_t* p = a.cnt_ce;
-  return W2Msg{p, p + m1, p + 2 * m1, p + 3 * m1, p + 4 * m1, p + 5 * m1, p + 6 * m1, a.cnt_o};
+  return W2Msg{p, p + m1, p + 2 * m1, p + 3 * m1, p + 4 * m1, p + 5 * m1, p + 6 * m1, a.cnt_o, a.inl};
 }
 
 // grid of the grid-stride certificate-entry kernels (the entry total is on the device)
