@@ -878,13 +878,14 @@ int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_
   a->ce = cnt + (size_t)mochi::kW2MsgArrays * m1;
   a->ce_cap = mochi::kW2MaxCertEntries * (uint32_t)m1;
   a->inl = (uint32_t*)(((uintptr_t)(a->ce + 11 * (size_t)a->ce_cap) + 15) & ~(uintptr_t)15);
+  a->cnt4 = a->inl + 4 * (size_t)mochi::kW2InlEntries * m1;
+  a->off4 = a->cnt4 + 4 * m1;
   a->status = status;
   a->scan_temp = c->w2_scan.p;
   a->scan_temp_bytes = c->w2_scan.cap;
   HIP_TRY(mochi::launch_w2_count(*a, st));
-  HIP_TRY(hipMemcpyAsync(tot_host, a->cert_grant_off + M, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(tot_host + 1, a->cert_op_off + M, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(tot_host + 2, a->cert_mg_off + M, 4, hipMemcpyDeviceToHost, st));
+  // decoded grants, ops and MultiGrants: the packed scan's last element
+  HIP_TRY(hipMemcpyAsync(tot_host, a->off4 + 4 * (size_t)M, 12, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipEventRecord(ev_tot, st));
   return MOCHI_OK;
 }

@@ -31,6 +31,8 @@ struct W2Args {
   uint32_t* ce;
   uint32_t ce_cap;
   uint32_t* inl;  // [M+1][kW2InlEntries][4], 16-byte aligned: level 1's first entries (key / value slices)
+  uint32_t* cnt4;  // [M+1][4], 16-byte aligned: decoded grants, ops, MultiGrants per message (one scan)
+  uint32_t* off4;  // [M+1][4]: their exclusive scan (unpacked into cert_*_off by k_w2_ops)
   uint8_t* status;  // [M]
   void* scan_temp;
   size_t scan_temp_bytes;
@@ -53,7 +55,8 @@ struct W2Args {
 };
 // Device words of one decode's per-batch scratch: 13 arrays of M+1 (counts,
 // CSR offsets, level-1 state) + the certificate-entry list (at most
-// kW2MaxCertEntries per message on the fast path, 11 words each).
+// kW2MaxCertEntries per message on the fast path, 11 words each) + level 1's
+// entry records + the packed per-message counts and their scan.
 constexpr uint32_t kW2MaxCertEntries = 32;
 constexpr int kW2MsgArrays = 13;
 // Level 1 records the key / value slices of a message's first kW2InlEntries
@@ -61,7 +64,7 @@ constexpr int kW2MsgArrays = 13;
 constexpr uint32_t kW2InlEntries = 4;
 inline size_t w2_scratch_words(uint32_t M) {
   return (size_t)kW2MsgArrays * ((size_t)M + 1) + 11 * (size_t)kW2MaxCertEntries * ((size_t)M + 1) +
-         4 * (size_t)kW2InlEntries * ((size_t)M + 1) + 4;  // + 4: the records start 16-byte aligned
+         4 * (size_t)kW2InlEntries * ((size_t)M + 1) + 8 * ((size_t)M + 1) + 4;  // + 4: 16-byte alignment
 }
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
 hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans

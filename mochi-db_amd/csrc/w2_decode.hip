@@ -990,13 +990,14 @@ __global__ __launch_bounds__(256) void k_w2_mg(
 // Per message: final status and the decoded counts.
 __global__ __launch_bounds__(256) void k_w2_final(uint32_t M, const uint32_t* __restrict__ flags_off, W2Msg s, CE ce,
                                                   uint32_t* __restrict__ cnt_g, uint32_t* __restrict__ cnt_m,
-                                                  uint8_t* __restrict__ status) {
+                                                  uint8_t* __restrict__ status, uint4* __restrict__ cnt4) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m > M) return;
-  if (m == M) {  // the scans' extra element: totals land at [M]
+  if (m == M) {  // the scan's extra element: totals land at [M]
     cnt_g[M] = 0;
     s.cnt_o[M] = 0;
     cnt_m[M] = 0;
+    cnt4[M] = make_uint4(0, 0, 0, 0);
     return;
   }
   const uint32_t bits = s.st_bits[m];
@@ -1018,6 +1019,7 @@ __global__ __launch_bounds__(256) void k_w2_final(uint32_t M, const uint32_t* __
   cnt_g[m] = ng;
   s.cnt_o[m] = no;
   cnt_m[m] = nm;
+  cnt4[m] = make_uint4(ng, no, nm, 0);
   status[m] = (uint8_t)st;
 }
 
@@ -1026,8 +1028,7 @@ __global__ __launch_bounds__(256) void k_w2_final(uint32_t M, const uint32_t* __
 __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
                                                     const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce,
                                                     const uint8_t* __restrict__ status,
-                                                    const uint32_t* __restrict__ g_base,
-                                                    const uint32_t* __restrict__ m_base, const uint8_t* __restrict__ ids,
+                                                    const uint4* __restrict__ off4, const uint8_t* __restrict__ ids,
                                                     const uint32_t* __restrict__ id_off, uint32_t n_ids, W2Out out) {
   const uint32_t total = s.ce_base[M];
 #pragma unroll 1
@@ -1045,8 +1046,9 @@ __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ 
         gb += ce.ng[Lj];
       }
     }
-    uint32_t g = g_base[m] + gb;
-    out.mg_grant_off[m_base[m] + idx] = g;  // this MultiGrant's first grant
+    const uint4 base = off4[m];  // (grants, ops, MultiGrants) before message m
+    uint32_t g = base.x + gb;
+    out.mg_grant_off[base.z + idx] = g;  // this MultiGrant's first grant
     const uint64_t mo = moff[m];
     if (ce.ng[L] == 1) {  // recorded by k_w2_mg
       const uint32_t sk = ce.r_sk[L];
@@ -1066,18 +1068,27 @@ __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ 
 // naming the same operand1) and the MultiGrant CSR terminator.
 __global__ __launch_bounds__(256) void k_w2_ops(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
                                                 const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s,
-                                                const uint8_t* __restrict__ status, const uint32_t* __restrict__ g_base,
-                                                const uint32_t* __restrict__ o_base, const uint32_t* __restrict__ m_base,
-                                                const uint32_t* __restrict__ flags_off,
+                                                const uint8_t* __restrict__ status, const uint4* __restrict__ off4,
+                                                uint32_t* __restrict__ g_base, uint32_t* __restrict__ o_base,
+                                                uint32_t* __restrict__ m_base, const uint32_t* __restrict__ flags_off,
                                                 const uint8_t* __restrict__ flags_in,
                                                 const int64_t* __restrict__ ots_in, W2Out out) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m == 0) out.mg_grant_off[m_base[M]] = g_base[M];  // CSR terminator: n_mgs -> N
-  if (m >= M || status[m] != MOCHI_MSG_OK) return;
+  if (m > M) return;
+  // the packed scan unpacked into the batch's three CSR arrays ([M] = totals)
+  const uint4 base = off4[m];
+  g_base[m] = base.x;
+  o_base[m] = base.y;
+  m_base[m] = base.z;
+  if (m == M) {
+    out.mg_grant_off[base.z] = base.x;  // CSR terminator: n_mgs -> N
+    return;
+  }
+  if (status[m] != MOCHI_MSG_OK) return;
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
   const uint64_t msg_off = moff[m];
-  const uint32_t ob = o_base[m], tx_off = s.tx_off[m], end = tx_off + s.tx_len[m];
+  const uint32_t ob = base.y, tx_off = s.tx_off[m], end = tx_off + s.tx_len[m];
   const uint8_t* fl = flags_off ? flags_in + flags_off[m] : nullptr;
   const int64_t* ot = flags_off && ots_in ? ots_in + flags_off[m] : nullptr;
   uint32_t no = 0, pos = tx_off;
@@ -1189,8 +1200,20 @@ inline uint32_t ce_blocks(const W2Args& a) {
 
 }  // namespace
 
+struct Sum4 {
+  __host__ __device__ uint4 operator()(const uint4& a, const uint4& b) const {
+    return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+};
+
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes) {
-  return hipcub::DeviceScan::ExclusiveSum(nullptr, *bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  size_t b1 = 0, b4 = 0;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, b1, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceScan::ExclusiveScan(nullptr, b4, (const uint4*)nullptr, (uint4*)nullptr, Sum4{},
+                                        make_uint4(0, 0, 0, 0), (int)n);
+  *bytes = b1 > b4 ? b1 : b4;
+  return e;
 }
 
 hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
@@ -1208,17 +1231,14 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
     hipLaunchKernelGGL(k_w2_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce, a.ids,
                        a.id_off, a.n_ids);
   }
-  hipLaunchKernelGGL(k_w2_final, dim3(gm1), dim3(256), 0, st, a.M, a.flags_off, s, ce, a.cnt_g, a.cnt_m, a.status);
+  hipLaunchKernelGGL(k_w2_final, dim3(gm1), dim3(256), 0, st, a.M, a.flags_off, s, ce, a.cnt_g, a.cnt_m, a.status,
+                     (uint4*)a.cnt4);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // one scan of the packed (grants, ops, MultiGrants) counts instead of three
   tb = a.scan_temp_bytes;
-  e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_g, a.cert_grant_off, (int)(a.M + 1), st);
-  if (e != hipSuccess) return e;
-  tb = a.scan_temp_bytes;
-  e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_o, a.cert_op_off, (int)(a.M + 1), st);
-  if (e != hipSuccess) return e;
-  tb = a.scan_temp_bytes;
-  return hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.cnt_m, a.cert_mg_off, (int)(a.M + 1), st);
+  return hipcub::DeviceScan::ExclusiveScan(a.scan_temp, tb, (const uint4*)a.cnt4, (uint4*)a.off4, Sum4{},
+                                           make_uint4(0, 0, 0, 0), (int)(a.M + 1), st);
 }
 
 hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
@@ -1228,9 +1248,10 @@ hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
   const CE ce = ce_view(a.ce, a.ce_cap);
   if (a.M)
     hipLaunchKernelGGL(k_w2_emit_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce,
-                       a.status, a.cert_grant_off, a.cert_mg_off, a.ids, a.id_off, a.n_ids, o);
-  hipLaunchKernelGGL(k_w2_ops, dim3(cdiv(a.M ? a.M : 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s,
-                     a.status, a.cert_grant_off, a.cert_op_off, a.cert_mg_off, a.flags_off, a.flags_in, a.ots_in, o);
+                       a.status, (const uint4*)a.off4, a.ids, a.id_off, a.n_ids, o);
+  hipLaunchKernelGGL(k_w2_ops, dim3(cdiv((uint64_t)a.M + 1, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len,
+                     a.M, s, a.status, (const uint4*)a.off4, a.cert_grant_off, a.cert_op_off, a.cert_mg_off,
+                     a.flags_off, a.flags_in, a.ots_in, o);
   if (a.N) hipLaunchKernelGGL(k_w2_sig, dim3(cdiv((uint64_t)a.N * 16, 256)), dim3(256), 0, st, a.wire, a.sig_src, a.N, a.sig);
   return hipGetLastError();
 }
