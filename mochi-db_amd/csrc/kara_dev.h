@@ -19,6 +19,10 @@
 #include "fold.h"
 #include "mont.h"
 
+#ifndef MOCHI_PIN_PRODUCT
+#define MOCHI_PIN_PRODUCT 0
+#endif
+
 namespace mochi {
 
 constexpr int kKH = kL / 2;  // 37: the Karatsuba split
@@ -39,6 +43,9 @@ __device__ __forceinline__ void half_product(const uint32_t (&a)[NA], const uint
     static_for<lo, hi + 1>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       acc = mad64(a[AO + i], b[BO + k - i], acc);
+#if MOCHI_PIN_PRODUCT
+      asm volatile("" ::"v"(acc));  // one chain from the carry (see half_square)
+#endif
     });
     emit(std::integral_constant<int, k>{}, (uint32_t)acc & kLimbMask);
     carry = acc >> kLimbBits;
@@ -58,11 +65,10 @@ __device__ __forceinline__ void half_product(const uint32_t (&a)[NA], const uint
 // s_nop per squaring).  a_m is needed undoubled only up to column 2m (as the
 // higher index of a cross product, or squared) and doubled only after it (as
 // the lower index), so it is doubled IN PLACE right after column 2m: no extra
-// registers, 36 v_lshlrev per square; `a` is clobbered.  hipcc still sums each
-// column's products from zero and adds the carry with one v_lshl_add_u64
-// (re-association).  Bound: limbs of a are < 2^29 (M's a_lo + a_hi), so 2a_i <
-// 2^30, a product < 2^59, and a column < 18 * 2^59 + 2^58 + carry (< 2^36) <
-// 2^64 (tests/fold_model.py asserts every column).
+// registers, 36 v_lshlrev per square; `a` is clobbered.  Bound: limbs of a
+// are < 2^29 (M's a_lo + a_hi), so 2a_i < 2^30, a product < 2^59, and a column
+// < 18 * 2^59 + 2^58 + carry (< 2^36) < 2^64 (tests/fold_model.py asserts every
+// column).
 template <int AO, int NA, typename EMIT>
 __device__ __forceinline__ void half_square(uint32_t (&a)[NA], EMIT&& emit) {
   uint64_t carry = 0;
@@ -74,6 +80,11 @@ __device__ __forceinline__ void half_square(uint32_t (&a)[NA], EMIT&& emit) {
     static_for<lo, xhi + 1>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       acc = mad64(a[AO + i], a[AO + k - i], acc);  // a[AO + i] is already 2 a_i
+      // every partial sum is an operand of an (empty, input-only) asm: with a
+      // second use it cannot be re-associated, so the column stays one chain
+      // from the carry -- no v_lshl_add_u64 to add the carry afterwards, and no
+      // hazard s_nop (that pad follows asm that DEFINES a register)
+      asm volatile("" ::"v"(acc));
     });
     if constexpr ((k & 1) == 0) {
       acc = mad64(a[AO + (k >> 1)], a[AO + (k >> 1)], acc);
