@@ -19,10 +19,6 @@
 #include "fold.h"
 #include "mont.h"
 
-#ifndef MOCHI_PIN_PRODUCT
-#define MOCHI_PIN_PRODUCT 0
-#endif
-
 namespace mochi {
 
 constexpr int kKH = kL / 2;  // 37: the Karatsuba split
@@ -43,9 +39,7 @@ __device__ __forceinline__ void half_product(const uint32_t (&a)[NA], const uint
     static_for<lo, hi + 1>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       acc = mad64(a[AO + i], b[BO + k - i], acc);
-#if MOCHI_PIN_PRODUCT
       asm volatile("" ::"v"(acc));  // one chain from the carry (see half_square)
-#endif
     });
     emit(std::integral_constant<int, k>{}, (uint32_t)acc & kLimbMask);
     carry = acc >> kLimbBits;
