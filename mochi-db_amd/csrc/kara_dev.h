@@ -26,99 +26,120 @@ static_assert(2 * kKH == kL, "even limb count");
 constexpr int kSignedLo = kKH;          // first t limb that may be negative
 constexpr int kSignedHi = 3 * kKH + 1;  // one past the last (t[111] = M_74 + H_37 >= 0, but unnormalised)
 
-// Normalised limbs 0..74 of a 37 x 37 product a * b: emit(k, limb) in order.
-// AO / BO: the halves' offsets.
-template <int AO, int BO, int NA, int NB, typename EMIT>
-__device__ __forceinline__ void half_product(const uint32_t (&a)[NA], const uint32_t (&b)[NB], EMIT&& emit) {
-  uint64_t carry = 0;
-  static_for<0, 2 * kKH - 1>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    constexpr int lo = k - kKH + 1 > 0 ? k - kKH + 1 : 0;
-    constexpr int hi = k < kKH - 1 ? k : kKH - 1;
+// Column K (0..74) of a 37 x 37 product a * b, normalised; `carry` runs from
+// column to column (columns 73 and 74 are the last carry's two limbs).  AO / BO:
+// the halves' offsets.
+template <int AO, int BO, int K, int NA, int NB>
+__device__ __forceinline__ uint32_t product_col(const uint32_t (&a)[NA], const uint32_t (&b)[NB], uint64_t& carry) {
+  if constexpr (K == 2 * kKH - 1) {
+    return (uint32_t)carry & kLimbMask;
+  } else if constexpr (K == 2 * kKH) {
+    return (uint32_t)(carry >> kLimbBits);
+  } else {
+    constexpr int lo = K - kKH + 1 > 0 ? K - kKH + 1 : 0;
+    constexpr int hi = K < kKH - 1 ? K : kKH - 1;
     uint64_t acc = carry;
     static_for<lo, hi + 1>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      acc = mad64(a[AO + i], b[BO + k - i], acc);
-      asm volatile("" ::"v"(acc));  // one chain from the carry (see half_square)
+      acc = mad64(a[AO + i], b[BO + K - i], acc);
+      asm volatile("" ::"v"(acc));  // one chain from the carry (see square_col)
     });
-    emit(std::integral_constant<int, k>{}, (uint32_t)acc & kLimbMask);
     carry = acc >> kLimbBits;
-    // column by column: left alone the scheduler hoists later columns' mads
-    // and keeps dozens of 64-bit column sums live
-    __builtin_amdgcn_sched_barrier(0);
-  });
-  emit(std::integral_constant<int, 2 * kKH - 1>{}, (uint32_t)carry & kLimbMask);
-  emit(std::integral_constant<int, 2 * kKH>{}, (uint32_t)(carry >> kLimbBits));
+    return (uint32_t)acc & kLimbMask;
+  }
 }
 
-// A 37-limb square, product-scanned with the doubling folded into the
-// operands: column k = carry + sum_{i < k-i} (2 a_i) a_{k-i} + a_{k/2}^2, one
-// chain of v_mad_u64_u32 with the square term in it (the schoolbook form sums
-// the cross products, doubles the sum with a v_lshl_add_u64 and needs an asm
-// barrier to keep hipcc from doubling every a_i, whose hazard pads cost ~250
-// s_nop per squaring).  a_m is needed undoubled only up to column 2m (as the
-// higher index of a cross product, or squared) and doubled only after it (as
-// the lower index), so it is doubled IN PLACE right after column 2m: no extra
-// registers, 36 v_lshlrev per square; `a` is clobbered.  Bound: limbs of a
-// are < 2^29 (M's a_lo + a_hi), so 2a_i < 2^30, a product < 2^59, and a column
-// < 18 * 2^59 + 2^58 + carry (< 2^36) < 2^64 (tests/fold_model.py asserts every
-// column).
-template <int AO, int NA, typename EMIT>
-__device__ __forceinline__ void half_square(uint32_t (&a)[NA], EMIT&& emit) {
-  uint64_t carry = 0;
-  static_for<0, 2 * kKH - 1>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    constexpr int lo = k - kKH + 1 > 0 ? k - kKH + 1 : 0;
-    constexpr int xhi = k > 0 ? (k - 1) / 2 : -1;
+// Column K of a 37-limb square, product-scanned with the doubling folded into
+// the operands: column k = carry + sum_{i < k-i} (2 a_i) a_{k-i} + a_{k/2}^2,
+// one chain of v_mad_u64_u32 with the square term in it (the schoolbook form
+// sums the cross products, doubles the sum with a v_lshl_add_u64 and needs an
+// asm barrier to keep hipcc from doubling every a_i, whose hazard pads cost
+// ~250 s_nop per squaring).  a_m is needed undoubled only up to column 2m (as
+// the higher index of a cross product, or squared) and doubled only after it
+// (as the lower index), so it is doubled IN PLACE right after column 2m: no
+// extra registers, 36 v_lshlrev per square; `a` is clobbered.  Bound: limbs of
+// a are < 2^29 (M's a_lo + a_hi), so 2a_i < 2^30, a product < 2^59, and a
+// column < 18 * 2^59 + 2^58 + carry (< 2^36) < 2^64 (tests/fold_model.py
+// asserts every column).
+template <int AO, int K, int NA>
+__device__ __forceinline__ uint32_t square_col(uint32_t (&a)[NA], uint64_t& carry) {
+  if constexpr (K == 2 * kKH - 1) {
+    return (uint32_t)carry & kLimbMask;
+  } else if constexpr (K == 2 * kKH) {
+    return (uint32_t)(carry >> kLimbBits);
+  } else {
+    constexpr int lo = K - kKH + 1 > 0 ? K - kKH + 1 : 0;
+    constexpr int xhi = K > 0 ? (K - 1) / 2 : -1;
     uint64_t acc = carry;
     static_for<lo, xhi + 1>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      acc = mad64(a[AO + i], a[AO + k - i], acc);  // a[AO + i] is already 2 a_i
+      acc = mad64(a[AO + i], a[AO + K - i], acc);  // a[AO + i] is already 2 a_i
       // every partial sum is an operand of an (empty, input-only) asm: with a
       // second use it cannot be re-associated, so the column stays one chain
       // from the carry -- no v_lshl_add_u64 to add the carry afterwards, and no
       // hazard s_nop (that pad follows asm that DEFINES a register)
       asm volatile("" ::"v"(acc));
     });
-    if constexpr ((k & 1) == 0) {
-      acc = mad64(a[AO + (k >> 1)], a[AO + (k >> 1)], acc);
-      if constexpr ((k >> 1) < kKH - 1) a[AO + (k >> 1)] += a[AO + (k >> 1)];
+    if constexpr ((K & 1) == 0) {
+      acc = mad64(a[AO + (K >> 1)], a[AO + (K >> 1)], acc);
+      if constexpr ((K >> 1) < kKH - 1) a[AO + (K >> 1)] += a[AO + (K >> 1)];
     }
-    emit(std::integral_constant<int, k>{}, (uint32_t)acc & kLimbMask);
     carry = acc >> kLimbBits;
-    __builtin_amdgcn_sched_barrier(0);  // column by column (see half_product)
+    return (uint32_t)acc & kLimbMask;
+  }
+}
+
+// M = (a_lo + a_hi)(b_lo + b_hi) (`col` gives its columns) straight into
+// t[37..111], column by column: left alone the scheduler hoists later columns'
+// mads and keeps dozens of 64-bit column sums live.
+template <typename COL>
+__device__ __forceinline__ void kara_middle(uint32_t (&t)[2 * kL], COL&& col) {
+  uint64_t carry = 0;
+  static_for<0, 2 * kKH + 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    t[kKH + k] = col(kc, carry);
+    __builtin_amdgcn_sched_barrier(0);
   });
-  emit(std::integral_constant<int, 2 * kKH - 1>{}, (uint32_t)carry & kLimbMask);
-  emit(std::integral_constant<int, 2 * kKH>{}, (uint32_t)(carry >> kLimbBits));
 }
 
 // The combination t = L + 2^(28*37) (M - L - H) + 2^(28*74) H once M is in
-// t[37..111]: L's limbs (run by `low`) and H's (run by `high`) are folded in as
-// their chains emit them -- no limb of L or H is stored.  t_hi (t[73..147])
-// leaves with its bytes 0..2 XOR kFoldBias (the fold's signed B operand),
-// applied where a limb is final.
+// t[37..111], written with Q = L - 2^(28*37) H as
+//     t_k = Q_k + M_(k-37) - Q_(k-37)
+// so each Q_k = L_k - H_(k-37) (k = 37..73) is formed once and used twice
+// (186 adds instead of 223).  The L chain (`low`) and the H chain (`high`) run
+// in lockstep, column c of L beside column c-37 of H -- two independent mad
+// chains per step for the scheduler to interleave -- and no limb of either is
+// stored.  t_hi (t[73..147]) leaves with its bytes 0..2 XOR kFoldBias (the
+// fold's signed B operand), applied where a limb is final.
 template <typename LOW, typename HIGH>
 __device__ __forceinline__ void kara_combine(uint32_t (&t)[2 * kL], LOW&& low, HIGH&& high) {
-  low([&](auto kc, uint32_t v) {  // t[k] (+)= L_k, t[37 + k] -= L_k
-    constexpr int k = decltype(kc)::value;
-    if constexpr (k < kL) {  // L_74 == 0
-      if constexpr (k < kKH) t[k] = v;
-      else t[k] += v;
-      t[kKH + k] -= v;
-    }
-  });
-  high([&](auto mc, uint32_t v) {  // t[37 + m] -= H_m, t[74 + m] (+)= H_m
-    constexpr int m = decltype(mc)::value;
-    if constexpr (m < kL) {  // H_74 == 0
-      t[kKH + m] -= v;
-      if constexpr (kKH + m >= kFoldF) t[kKH + m] ^= kFoldBias;  // its last update
-      if constexpr (m <= kKH) {
-        t[2 * kKH + m] += v;
-        if constexpr (m == kKH) t[2 * kKH + m] ^= kFoldBias;  // t[111]: final
+  uint64_t cl = 0, ch = 0;
+  static_for<0, 3 * kKH>([&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    if constexpr (c < kKH) {  // Q_c = L_c
+      const uint32_t l = low(cc, cl);
+      t[c] = l;
+      t[kKH + c] -= l;  // M_c - Q_c
+    } else if constexpr (c < kL) {  // Q_c = L_c - H_(c-37)
+      const uint32_t l = low(cc, cl);
+      const uint32_t h = high(std::integral_constant<int, c - kKH>{}, ch);
+      const uint32_t q = l - h;
+      t[c] += q;  // final: M_(c-37) - Q_(c-37) + Q_c
+      if constexpr (c >= kFoldF) t[c] ^= kFoldBias;
+      t[kKH + c] -= q;  // M_c - Q_c
+    } else {  // Q_c = -H_(c-37), and t_(c+37) = -Q_c = H_(c-37)
+      constexpr int m = c - kKH;
+      const uint32_t h = high(std::integral_constant<int, m>{}, ch);
+      t[c] -= h;  // final
+      t[c] ^= kFoldBias;
+      if constexpr (m == kKH) {
+        t[kKH + c] += h;  // t[111] = M_74 + H_37: final
+        t[kKH + c] ^= kFoldBias;
       } else {
-        t[2 * kKH + m] = v ^ kFoldBias;
+        t[kKH + c] = h ^ kFoldBias;
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
   });
 }
 
@@ -130,9 +151,11 @@ __device__ __forceinline__ void kara_square(uint32_t (&x)[kL], uint32_t (&t)[2 *
     uint32_t sx[kKH];
 #pragma unroll
     for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
-    half_square<0>(sx, [&](auto kc, uint32_t v) { t[kKH + decltype(kc)::value] = v; });
+    kara_middle(t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(sx, carry); });
   }
-  kara_combine(t, [&](auto&& emit) { half_square<0>(x, emit); }, [&](auto&& emit) { half_square<kKH>(x, emit); });
+  kara_combine(
+      t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(x, carry); },
+      [&](auto kc, uint64_t& carry) { return square_col<kKH, decltype(kc)::value>(x, carry); });
 }
 
 // t = x * y as 148 limbs (k_rsa_final), the same layout as kara_square.
@@ -144,10 +167,11 @@ __device__ __forceinline__ void kara_product(const uint32_t (&x)[kL], const uint
       sx[i] = x[i] + x[kKH + i];
       sy[i] = y[i] + y[kKH + i];
     }
-    half_product<0, 0>(sx, sy, [&](auto kc, uint32_t v) { t[kKH + decltype(kc)::value] = v; });
+    kara_middle(t, [&](auto kc, uint64_t& carry) { return product_col<0, 0, decltype(kc)::value>(sx, sy, carry); });
   }
-  kara_combine(t, [&](auto&& emit) { half_product<0, 0>(x, y, emit); },
-               [&](auto&& emit) { half_product<kKH, kKH>(x, y, emit); });
+  kara_combine(
+      t, [&](auto kc, uint64_t& carry) { return product_col<0, 0, decltype(kc)::value>(x, y, carry); },
+      [&](auto kc, uint64_t& carry) { return product_col<kKH, kKH, decltype(kc)::value>(x, y, carry); });
 }
 
 }  // namespace mochi
