@@ -51,10 +51,9 @@ constexpr int kHL = 10;  // a SHA-256 digest in radix 2^28
 typedef __attribute__((address_space(1))) char gchar;
 typedef __attribute__((address_space(1))) uint32_t guint;
 
-// BIASED: t_hi limbs (t[kFoldF..]) arrive already XOR kFoldBias.
-// SIGNED_LO: t_lo limbs from kSignedLo (37) on are signed int32 (kara_dev.h)
-// and join the 64-bit carry chain on their own instead of the int32 sum.
-template <bool SUB_H, bool BIASED = false, bool SIGNED_LO = false>
+// BIASED: t_hi limbs (t[kFoldF..]) arrive already XOR kFoldBias.  t_lo limbs
+// may be signed (Karatsuba's t[37..72], |t| < 2^29: kara_dev.h).
+template <bool SUB_H, bool BIASED = false>
 __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_t (&x)[kL],
                                             const v4i* __restrict__ wl, cptr cadd, const uint32_t* hl) {
   // tile 0's first A fragment: issued before the B operands are formed (their
@@ -110,18 +109,17 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
       constexpr int q = 8 * mt + r, u = r >> 1;
       if constexpr (q < kL) {
         // limb q = c0 + 2^8 c1 + 2^16 (c2 + 2^8 c3) + t_lo + cadd (- h) + carry;
-        // the first terms of p stay in int32 (|c0 + 2^8 c1| < 1.27e9, normalised
-        // t_lo, cadd and h < 2^28), h * 2^16 + p + carry is two v_mad_i64_i32
-        // (three for a signed t_lo limb, up to +-2^29, which could overflow p)
-        constexpr bool lo_signed = SIGNED_LO && q >= kSignedLo && q < kFoldF;
+        // p = c0 + 2^8 c1 + t_lo + cadd (- h) stays in int32: |c0 + 2^8 c1| <=
+        // 257 * 300 * 2^14 = 1,263,206,400, |t_lo| < 2^29 (signed Karatsuba
+        // limbs), cadd and h < 2^28, so -1.80e9 < p < 2.07e9 < 2^31
+        // (tests/fold_model.py asserts it); h * 2^16 + p + carry is two
+        // v_mad_i64_i32
         int p = (r & 1) ? p1[u] : p0[u];
-        if constexpr (q < kFoldF && !lo_signed) p += (int)t[q];
+        if constexpr (q < kFoldF) p += (int)t[q];
         p += (int)cadd[q];
         if constexpr (SUB_H && q < kHL) p -= (int)hl[q];
         const int h = (r & 1) ? h1[u] : h0[u];
-        int64_t c = carry;
-        if constexpr (lo_signed) c = mad_i64((int)t[q], 1, c);
-        const int64_t v = mad_i64(h, 65536, mad_i64(p, 1, c));
+        const int64_t v = mad_i64(h, 65536, mad_i64(p, 1, carry));
         x[q] = (uint32_t)v & kLimbMask;
         carry = v >> kLimbBits;
       }

@@ -23,8 +23,6 @@ namespace mochi {
 
 constexpr int kKH = kL / 2;  // 37: the Karatsuba split
 static_assert(2 * kKH == kL, "even limb count");
-constexpr int kSignedLo = kKH;          // first t limb that may be negative
-constexpr int kSignedHi = 3 * kKH + 1;  // one past the last (t[111] = M_74 + H_37 >= 0, but unnormalised)
 
 // Column K (0..74) of a 37 x 37 product a * b, normalised; `carry` runs from
 // column to column (columns 73 and 74 are the last carry's two limbs).  AO / BO:

@@ -87,7 +87,7 @@ __device__ __forceinline__ void final_slot(uint32_t slot, uint32_t base, uint32_
     }
   }
   // ---- D = t_lo + fold(t_hi) + cadd + n - Cpad - H ----
-  fold_reduce<true, true, true>(t, x, w + (threadIdx.x & 63), as_const(fold[key].cnc), hl);
+  fold_reduce<true, true>(t, x, w + (threadIdx.x & 63), as_const(fold[key].cnc), hl);
   // ---- D' = (D + m n) / 2^28 == n ? ----
   cptr nn = n;
   asm volatile("" : "+s"(nn));  // reload n here (kept from the s < n check it would sit in SGPRs and spill)

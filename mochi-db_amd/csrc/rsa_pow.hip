@@ -58,7 +58,7 @@ __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restric
   const uint64_t t0 = stamp();
   kara_square(x, t);  // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
   const uint64_t t1 = stamp();
-  fold_reduce<false, true, true>(t, x, wl, cadd, nullptr);
+  fold_reduce<false, true>(t, x, wl, cadd, nullptr);
   const uint64_t t2 = stamp();
   st.x2 += t1 - t0;
   st.fold += t2 - t1;

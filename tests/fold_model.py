@@ -111,8 +111,10 @@ def _columns(a, b, sqr):
 
 def kara_terms(a, b=None):
     """t = a*b (a*a if b is None), 74-limb operands, as 148 signed limbs: the
-    kernel's one-level Karatsuba with its order of operations (M, then L, then H)
-    and no normalisation of the combination, t[37..111] in (-2^29, 2^29)."""
+    kernel's one-level Karatsuba with its order of operations (M into t[37..111],
+    then the L and H chains in lockstep, t_k = Q_k + M_(k-37) - Q_(k-37) with
+    Q = L - 2^(28*37) H) and no normalisation of the combination, t[37..111] in
+    (-2^29, 2^29)."""
     sqr = b is None
     a0, a1 = list(a[:HALF]), list(a[HALF:])
     if sqr:
@@ -129,18 +131,21 @@ def kara_terms(a, b=None):
     t = [0] * (2 * L)
     for k in range(75):          # M_k -> t[37 + k]
         t[HALF + k] = M[k]
-    for k in range(74):          # L: t[k] (+)= L_k, t[37 + k] -= L_k
-        if k < HALF:
-            t[k] = Lw[k]
-        else:
-            t[k] += Lw[k]
-        t[HALF + k] -= Lw[k]
-    for m in range(74):          # H: t[37 + m] -= H_m, t[74 + m] (+)= H_m
-        t[HALF + m] -= Hw[m]
-        if m <= HALF:
-            t[2 * HALF + m] += Hw[m]
-        else:
-            t[2 * HALF + m] = Hw[m]
+    for c in range(3 * HALF):    # step c: L column c beside H column c - 37
+        if c < HALF:             # Q_c = L_c
+            t[c] = Lw[c]
+            t[HALF + c] -= Lw[c]
+        elif c < L:              # Q_c = L_c - H_(c-37), used twice
+            q = Lw[c] - Hw[c - HALF]
+            t[c] += q
+            t[HALF + c] -= q
+        else:                    # Q_c = -H_(c-37); t_(c+37) = H_(c-37)
+            m = c - HALF
+            t[c] -= Hw[m]
+            if m == HALF:
+                t[HALF + c] += Hw[m]
+            else:
+                t[HALF + c] = Hw[m]
     assert all(-(1 << 29) < v < (1 << 29) for v in t)
     av, bv = from_limbs(a), from_limbs(a if sqr else b)
     assert sum(v << (28 * k) for k, v in enumerate(t)) == av * bv
@@ -160,10 +165,11 @@ def fold_signed(t, W, cadd, sub_h=None):
     assert np.abs(c).max() < 2 ** 31
     out, carry = [], 0
     for q in range(L):
-        p = int(c[q, 0]) + (int(c[q, 1]) << 8) + int(cadd[q]) - (sub_h[q] if sub_h and q < len(sub_h) else 0)
+        p = int(c[q, 0]) + (int(c[q, 1]) << 8) + (t_lo[q] if q < F else 0) + int(cadd[q]) \
+            - (sub_h[q] if sub_h and q < len(sub_h) else 0)
         h = int(c[q, 2]) + (int(c[q, 3]) << 8)
         assert -2 ** 31 <= p < 2 ** 31 and -2 ** 31 <= h < 2 ** 31  # the kernel's int32 halves
-        v = (h << 16) + p + (t_lo[q] if q < F else 0) + carry
+        v = (h << 16) + p + carry
         out.append(v & M28)
         carry = v >> 28
     assert carry == 0
