@@ -34,12 +34,12 @@
 
 namespace mochi {
 #if MOCHI_POW_STAMPS
-__device__ unsigned long long g_pow_stamps[4096][4];
+__device__ unsigned long long g_pow_stamps[4096][5];
 #endif
 namespace {
 
 struct Stamps {
-  uint64_t x2 = 0, fold = 0, n = 0;
+  uint64_t x2 = 0, fold = 0, n = 0, mid = 0;
 };
 
 __device__ __forceinline__ uint64_t stamp() {
@@ -56,7 +56,20 @@ __device__ __forceinline__ uint64_t stamp() {
 __device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restrict__ wl, cptr cadd, Stamps& st) {
   uint32_t t[2 * kL];
   const uint64_t t0 = stamp();
+#if MOCHI_POW_STAMPS
+  {  // kara_square with a stamp after the middle product (M's one chain vs L and H in lockstep)
+    uint32_t sx[kKH];
+#pragma unroll
+    for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
+    kara_middle(t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(sx, carry); });
+  }
+  st.mid += stamp() - t0;
+  kara_combine(
+      t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(x, carry); },
+      [&](auto kc, uint64_t& carry) { return square_col<kKH, decltype(kc)::value>(x, carry); });
+#else
   kara_square(x, t);  // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
+#endif
   const uint64_t t1 = stamp();
   fold_reduce<false, true>(t, x, wl, cadd, nullptr);
   const uint64_t t2 = stamp();
@@ -107,6 +120,7 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const uint32_t* __restrict__
     g_pow_stamps[wv][1] = st.fold;
     g_pow_stamps[wv][2] = t_end - t_begin;
     g_pow_stamps[wv][3] = st.n;
+    g_pow_stamps[wv][4] = st.mid;
   }
 #else
   (void)t_begin;
@@ -118,7 +132,7 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const uint32_t* __restrict__
 #if MOCHI_POW_STAMPS
 extern "C" int mochi_debug_pow_stamps(unsigned long long* out, unsigned n_waves) {
   if (n_waves > 4096) n_waves = 4096;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pow_stamps), 32 * (size_t)n_waves, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pow_stamps), 40 * (size_t)n_waves, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -1,5 +1,5 @@
 """Phase times of k_rsa_pow from a MOCHI_POW_STAMPS build (MOCHI_HIP_LIB points
-at it): per wave, s_memtime cycles per squaring in x^2 and in the fold, and the
+at it): per wave, s_memtime cycles per squaring in x^2 (and its middle product M) and in the fold, and the
 kernel's cycles per squaring overall.  One JSON line."""
 import ctypes
 import json
@@ -28,14 +28,15 @@ for _ in range(3):
 torch.cuda.synchronize()
 ok = bool(np.array_equal(out.to_host().grant_flags, synth.expected_flags))
 lib = ctypes.CDLL(os.environ["MOCHI_HIP_LIB"])
-buf = (ctypes.c_ulonglong * (4096 * 4))()
+buf = (ctypes.c_ulonglong * (4096 * 5))()
 assert lib.mochi_debug_pow_stamps(buf, 2048) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 4)[:2048].astype(np.float64)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 5)[:2048].astype(np.float64)
 a = a[a[:, 3] > 0]
 n = a[:, 3]
 res = {"lib": os.path.basename(os.environ["MOCHI_HIP_LIB"]), "grants": synth.batch.n_grants, "flags_ok": ok,
        "waves": int(a.shape[0]), "squarings_per_wave": float(n.mean()),
        "x2_cyc_per_sq": round(float((a[:, 0] / n).mean()), 1), "fold_cyc_per_sq": round(float((a[:, 1] / n).mean()), 1),
+       "x2_middle_cyc_per_sq": round(float((a[:, 4] / n).mean()), 1),
        "kernel_cyc_per_sq": round(float((a[:, 2] / n).mean()), 1),
        "x2_p10_p90": [round(float(np.percentile(a[:, 0] / n, q)), 1) for q in (10, 90)],
        "fold_p10_p90": [round(float(np.percentile(a[:, 1] / n, q)), 1) for q in (10, 90)]}
