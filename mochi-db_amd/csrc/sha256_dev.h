@@ -20,6 +20,11 @@ static __constant__ uint32_t kSha256K[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 __device__ __forceinline__ uint32_t sha_rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// a ^ b ^ c in one v_bitop3_b32 (truth table 0x96; hipcc forms bitop3 for
+// ch / maj but leaves a three-way XOR as two v_xor_b32)
+__device__ __forceinline__ uint32_t sha_xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 // One compression of the 16 big-endian words w into h.
 __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[16]) {
@@ -31,15 +36,15 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[
       wt = w[t];
     } else {
       const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint32_t s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = sha_xor3(sha_rotr(w15, 7), sha_rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = sha_xor3(sha_rotr(w2, 17), sha_rotr(w2, 19), w2 >> 10);
       wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
       w[t & 15] = wt;
     }
-    const uint32_t S1 = sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25);
+    const uint32_t S1 = sha_xor3(sha_rotr(e, 6), sha_rotr(e, 11), sha_rotr(e, 25));
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
-    const uint32_t S0 = sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22);
+    const uint32_t S0 = sha_xor3(sha_rotr(a, 2), sha_rotr(a, 13), sha_rotr(a, 22));
     const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
     const uint32_t t2 = S0 + mj;
     hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
