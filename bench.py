@@ -91,28 +91,78 @@ def parse_args():
     return ap.parse_args()
 
 
-def timed_steps(step, steps, warmup, stream, dist=None):
-    """W untimed steps, then K steps bracketed by barrier + synchronize; returns
-    (event seconds, wall seconds) of this rank."""
+def timed_steps(step, steps, warmup, stream=None, dist=None, sync=None):
+    """W untimed steps, then K steps bracketed by barrier + synchronize on both
+    sides; returns (event seconds, wall seconds) of this rank.  With a CUDA
+    `stream` the event time comes from HIP events on it; without one (the CPU
+    rehearsal of the rank plumbing, tests/test_bench_ranks.py) it is the wall
+    time.  `sync` defaults to torch.cuda.synchronize."""
     import torch
 
+    if sync is None:
+        sync = torch.cuda.synchronize
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sync()
+    e0 = e1 = None
+    if stream is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    e0.record(stream)
+    if e0 is not None:
+        e0.record(stream)
     for _ in range(steps):
         step()
-    e1.record(stream)
-    torch.cuda.synchronize()
+    if e1 is not None:
+        e1.record(stream)
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / 1e3, time.perf_counter() - t0
+    sync()
+    wall = time.perf_counter() - t0
+    return (e0.elapsed_time(e1) / 1e3 if e0 is not None else wall), wall
+
+
+def rank_shard(total_grants, R, k, world, rank, shard_plan):
+    """This rank's certificate shard of the config's batch: libmochi_hip's plan
+    (contiguous, 32-aligned, so the per-rank verdict bitmaps concatenate word by
+    word after the all-gather).  Returns (C_total, plan, c_lo, c_hi); the rank
+    generates the SURVEY §8d stream from certificate c_lo on (first_cert)."""
+    import workload as W
+
+    C_total = W.n_certs_for_grants(total_grants, R, k)
+    plan = shard_plan(C_total, world)
+    return C_total, plan, int(plan[rank]), int(plan[rank + 1])
+
+
+def reduce_over_ranks(dist, ev_s, wall, ok, n_grants, device):
+    """MAX of the timed span over ranks (the job is as slow as its slowest
+    rank), AND of the per-rank correctness gates, SUM of the grants verified.
+    Returns (t_max, wall_max, all_ok, total_grants)."""
+    import torch
+
+    t = torch.tensor([ev_s, wall, 1.0 if ok else 0.0], dtype=torch.float64, device=device)
+    n_all = torch.tensor([n_grants], dtype=torch.int64, device=device)
+    if dist is not None:
+        tt = t[:2].clone()
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ok_t = t[2:].clone()
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        t = torch.cat([tt, ok_t])
+        dist.all_reduce(n_all)
+    return float(t[0]), float(t[1]), bool(t[2] >= 1.0), int(n_all.item())
+
+
+def gathered_matches_rank0(plan, gathered_words, C_total, local_accept, bits_assemble, unpack_bits):
+    """Rank 0's check of the all-gather: the whole batch's bitmap, assembled from
+    the gathered per-rank slots, holds rank 0's own shard verdicts."""
+    import numpy as np
+
+    g = bits_assemble(plan, np.ascontiguousarray(gathered_words).view(np.uint32))
+    C0 = int(plan[1]) - int(plan[0])
+    return bool(np.array_equal(unpack_bits(g, C_total)[:C0], np.asarray(local_accept)[:C0]))
 
 
 def roofline(n_grants, pow_ms, traffic=None):
@@ -160,11 +210,7 @@ def main():
     R, k = args.replication or cfg["R"], args.ops_per_txn
     strict = not args.client_predicate
     total_grants = args.grants_total or cfg["grants"]
-    C_total = W.n_certs_for_grants(total_grants, R, k)
-    # this rank's certificate shard: libmochi_hip's plan (contiguous, 32-aligned, so the
-    # per-rank verdict bitmaps concatenate word by word after the all-gather)
-    plan = mh.shard_plan(C_total, world)
-    c_lo, c_hi = int(plan[rank]), int(plan[rank + 1])
+    C_total, plan, c_lo, c_hi = rank_shard(total_grants, R, k, world, rank, mh.shard_plan)
     C = c_hi - c_lo
     # CPU baseline (rank 0, N = 1 only): a child process started BEFORE this
     # process touches the GPU (it forks its workers and must hold no HIP
@@ -235,18 +281,7 @@ def main():
     ver.set_profiling(False)
     prof = ver.read_profile()
     stage_ms = [prof[name] for name in ver.STAGES]
-    t = torch.tensor([ev_s, wall, 1.0 if flags_ok else 0.0], dtype=torch.float64, device="cuda")
-    if dist is not None:
-        tt = t.clone()
-        dist.all_reduce(tt[:2], op=dist.ReduceOp.MAX)
-        ok_t = t[2:].clone()
-        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-        t = torch.cat([tt[:2], ok_t])
-    t_max, wall_max, all_ok = float(t[0]), float(t[1]), bool(t[2] >= 1.0)
-    n_all = torch.tensor([N], dtype=torch.int64, device="cuda")
-    if dist is not None:
-        dist.all_reduce(n_all)
-    total_grants_verified = int(n_all.item())
+    t_max, wall_max, all_ok, total_grants_verified = reduce_over_ranks(dist, ev_s, wall, flags_ok, N, "cuda")
     value = total_grants_verified * args.steps / t_max
 
     result = None
@@ -328,9 +363,8 @@ def main():
     if dist is not None:
         # the gathered bitmap is the whole batch's: rank 0 checks it holds its own shard's verdicts
         if rank == 0 and result is not None:
-            g = mh.bits_assemble(plan, gathered.cpu().numpy().view(np.uint32))
-            result["gathered_bitmap_matches_rank0"] = bool(np.array_equal(
-                mh.unpack_bits(g, C_total)[:C], host.cert_accept[:C]))
+            result["gathered_bitmap_matches_rank0"] = gathered_matches_rank0(
+                plan, gathered.cpu().numpy(), C_total, host.cert_accept, mh.bits_assemble, mh.unpack_bits)
         dist.barrier()
         comm.close()
         dist.destroy_process_group()
@@ -609,8 +643,11 @@ def batcher_async_leg(vers, wb, cert_grant_off, R, strict, ref, n_req=100000, wi
             "note": "one Python producer thread (ctypes call + callback per request bound the rate)"}
 
 
-NATIVE_CONFIGS = ["sync:2:1::20000", "sync:20:1::40000", "sync:20:2::40000", "sync:64:2::100000",
-                  "async:4:2:16384:400000"]
+# the reference's Write2 pool is core 2 / max 20 on an unbounded queue (MochiServer.java:36-39,51-52),
+# so it runs 2 workers: sync:2 is the blocking drop-in at that concurrency, async:2 the same 2 workers
+# submitting and completing each request from the callback (INTEGRATION.md's handler form)
+NATIVE_CONFIGS = ["sync:2:1::20000", "sync:2:2::20000", "async:2:1:16384:400000", "async:2:2:16384:400000",
+                  "sync:20:1::40000", "sync:20:2::40000", "sync:64:2::100000", "async:4:2:16384:400000"]
 
 
 def start_batcher_native(args, input_path):

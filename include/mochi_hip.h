@@ -551,11 +551,13 @@ typedef struct mochi_write2_request {
  * it.  This is the call a server's Write2 handler makes in place of
  * InMemoryDataStore.processWrite2ToServer (InMemoryDataStore.java:641-666): the
  * per-op decision says which operations applyOperation / readOperation runs.
- * MOCHI_EINVAL from a completion callback running on this batcher. */
+ * MOCHI_EINVAL (and mochi_last_error) from a completion callback running on
+ * this batcher: a callback submits instead. */
 int mochi_batcher_verify_request(mochi_batcher* b, const mochi_write2_request* req, mochi_verdict1* out);
 /* Non-blocking form: cb(user, rc, &verdict) runs on a flusher thread once the
- * batch is verified, after the per-op outputs are written.  Callbacks must not
- * call mochi_batcher_destroy / _verify* on the batcher running them. */
+ * batch is verified, after the per-op outputs are written.  A callback may
+ * submit to the batcher running it (e.g. the next stage of a future chain);
+ * _verify* from a callback returns MOCHI_EINVAL. */
 int mochi_batcher_submit_request(mochi_batcher* b, const mochi_write2_request* req, mochi_verdict_cb cb, void* user);
 /* Blocks until this message's verdict is in `out`.  Thread-safe.  Returns the
  * status of the batch call that carried it. */
@@ -570,8 +572,11 @@ int mochi_batcher_verify(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len,
 int mochi_batcher_submit(mochi_batcher* b, const uint8_t* msg, uint32_t msg_len, const uint8_t* op_flags,
                          uint32_t n_ops, const uint8_t* expected_hash, mochi_verdict_cb cb, void* user);
 int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs);
-/* Drains pending requests, then stops the flushers.  Not from a callback of
- * the same batcher (ignored there: the flusher would have to join itself). */
+/* Drains pending requests, then stops the flushers and frees the batcher once
+ * every blocked caller has returned.  From one of the batcher's own callbacks
+ * the teardown is deferred instead: later submissions are refused with
+ * MOCHI_EINVAL, requests already queued still complete, and the last flusher
+ * frees the batcher; the handle must not be used after the call either way. */
 void mochi_batcher_destroy(mochi_batcher* b);
 
 /* ------------------------------------------------------------------------

@@ -23,10 +23,15 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/mochi_hip.h"
+
+namespace mochi {
+int set_error(int code, const std::string& msg);  // capi.cpp: the text mochi_last_error() returns
+}
 
 namespace {
 
@@ -89,6 +94,9 @@ struct mochi_batcher {
   std::condition_variable cv_work, cv_done;
   std::deque<Request*> q;
   bool stop = false;
+  bool deferred_delete = false;  // destroyed from one of its own callbacks: the last flusher out frees it
+  uint32_t live = 0;             // flusher threads still in run()
+  uint32_t waiters = 0;          // blocking callers not yet out of their wait (mu is theirs until then)
   uint64_t n_batches = 0, n_msgs = 0;
   std::vector<Flusher> fl;
 
@@ -134,6 +142,17 @@ struct mochi_batcher {
       }
       cv_done.notify_all();
       for (Request* r : owned) delete r;
+    }
+    bool last;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      last = --live == 0 && deferred_delete;
+      if (last) cv_done.wait(lk, [&] { return waiters == 0; });
+    }
+    if (last) {  // mochi_batcher_destroy ran inside a callback: nobody will join us
+      t_flushing = nullptr;
+      for (auto& g : fl) g.th.detach();
+      delete this;
     }
   }
 
@@ -233,7 +252,6 @@ struct mochi_batcher {
                       : (r->op_flags != nullptr || r->n_ops != 0 || r->op_object_ts || r->op_decision || r->op_g0 ||
                          r->op_ts))
       return MOCHI_EINVAL;
-    if (t_flushing == this) return MOCHI_EINVAL;  // from a callback this batcher is running
     return MOCHI_OK;
   }
 
@@ -257,6 +275,7 @@ mochi_batcher* mochi_batcher_create_multi(mochi_ctx* const* ctxs, uint32_t n_ctx
   b->max_msgs = max_msgs;
   b->max_wait_us = max_wait_us;
   b->fl.resize(n_ctx);
+  b->live = n_ctx;
   for (uint32_t i = 0; i < n_ctx; i++) b->fl[i].ctx = ctxs[i];
   for (auto& f : b->fl) {
     Flusher* fp = &f;
@@ -274,6 +293,12 @@ int mochi_batcher_verify_request(mochi_batcher* b, const mochi_write2_request* r
   if (!b || !out) return MOCHI_EINVAL;
   int rc = b->check(req);
   if (rc) return rc;
+  // a callback blocking on the batcher that runs it would wait for itself
+  // (one flusher) or stall a flusher the others may be counting on; submitting
+  // from a callback is fine (enqueue only takes mu, which verify() has released)
+  if (t_flushing == b)
+    return mochi::set_error(MOCHI_EINVAL, "mochi_batcher_verify*: called from a completion callback of the same batcher; "
+                                          "use mochi_batcher_submit* there");
   Request r;
   r.r = *req;
   r.out = out;
@@ -283,7 +308,9 @@ int mochi_batcher_verify_request(mochi_batcher* b, const mochi_write2_request* r
   std::unique_lock<std::mutex> lk(b->mu);
   if (b->stop) return MOCHI_EINVAL;
   b->enqueue(&r);
+  b->waiters++;
   b->cv_done.wait(lk, [&] { return r.done; });
+  if (--b->waiters == 0 && b->stop) b->cv_done.notify_all();  // a destroy may be waiting for us
   return r.rc;
 }
 
@@ -339,7 +366,19 @@ int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs) {
 }
 
 void mochi_batcher_destroy(mochi_batcher* b) {
-  if (!b || t_flushing == b) return;  // never from one of its own callbacks (it would join itself)
+  if (!b) return;
+  if (t_flushing == b) {
+    // from one of its own callbacks: the flusher cannot join itself, so the
+    // teardown is deferred -- new submissions are refused from now on, the
+    // queue drains as usual, and the last flusher to leave frees the batcher
+    {
+      std::lock_guard<std::mutex> lk(b->mu);
+      b->stop = true;
+      b->deferred_delete = true;
+    }
+    b->cv_work.notify_all();
+    return;
+  }
   {
     std::lock_guard<std::mutex> lk(b->mu);
     b->stop = true;
@@ -347,6 +386,10 @@ void mochi_batcher_destroy(mochi_batcher* b) {
   b->cv_work.notify_all();
   for (auto& f : b->fl)
     if (f.th.joinable()) f.th.join();
+  {
+    std::unique_lock<std::mutex> lk(b->mu);
+    b->cv_done.wait(lk, [&] { return b->waiters == 0; });  // served callers still leaving their wait
+  }
   delete b;
 }
 

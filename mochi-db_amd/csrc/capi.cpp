@@ -46,6 +46,17 @@ bool prep_serial() {
   return v;
 }
 
+// MOCHI_PREP_KERNEL=1 (A/B and standalone timing): grant prep as its own kernel,
+// beside k_rsa_pow on the aux stream (serialised with MOCHI_PREP_SERIAL=1),
+// instead of inside k_rsa_pow's idle half-phases
+bool prep_kernel() {
+  static const bool v = [] {
+    const char* e = getenv("MOCHI_PREP_KERNEL");
+    return (e && atoi(e) != 0) || prep_serial();
+  }();
+  return v;
+}
+
 uint32_t default_chunk_grants() {
   const char* e = getenv("MOCHI_CHUNK_GRANTS");
   const long x = e ? atol(e) : 0;
@@ -289,19 +300,42 @@ struct mochi_ctx {
   // multi.cpp all-gathers it in place of re-uploading the host bits
   const uint32_t* acc_dev = nullptr;
   uint32_t acc_words = 0;
+  uint64_t gen = 0;  // bumped (under mu) by every call that may rewrite dev_out / scratch
   // per-stage profiling (mochi_ctx_set_profiling): one event set per verify call
   bool profiling = false;
   std::vector<std::vector<hipEvent_t>> prof_sets;
 };
 
 namespace mochi {
-const uint32_t* ctx_last_accept_dev(mochi_ctx* c, uint32_t* words, int* device, hipStream_t* stream) {
-  *words = c->acc_words;
-  *device = c->device;
-  *stream = c->stream;
-  return c->acc_dev;
+// the generation of the last context call made by this thread (multi.cpp reads it
+// right after its mochi_verify_* returns, on the same thread)
+thread_local uint64_t t_ctx_gen = 0;
+uint64_t ctx_call_gen() { return t_ctx_gen; }
+
+// Copies the certificate accept bitmap of context call `gen` from the device
+// (where that call left it) into dst on `st`, holding the context's lock until
+// the copy is done, so no later call can grow or overwrite dev_out under it.
+// 1 = not available (a later call ran, the call's device bitmap is not final,
+// or it lives on another device): the caller uploads its host bits instead.
+int ctx_copy_accept_dev(mochi_ctx* c, uint64_t gen, int device, uint32_t* dst, uint32_t need, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->gen != gen || !c->acc_dev || c->device != device || c->acc_words < need) return 1;
+  if (hipMemcpyAsync(dst, c->acc_dev, 4 * (size_t)need, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return MOCHI_EHIP;
+  return MOCHI_OK;
 }
 }  // namespace mochi
+
+namespace {
+// every entry point that launches on the context's buffers, with c->mu held
+void new_call(mochi_ctx* c) {
+  c->gen++;
+  c->acc_dev = nullptr;
+  c->acc_words = 0;
+  mochi::t_ctx_gen = c->gen;
+}
+}  // namespace
 
 extern "C" {
 
@@ -542,6 +576,7 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.op_ts = o->op_ts;
   a.op_out_off = op_out_off;
   a.aux = prep_serial() ? nullptr : c->aux;  // MOCHI_PREP_SERIAL=1: prep on the launch stream (A/B)
+  a.prep_kernel = prep_kernel();
   a.ev_fork = c->ev_fork;
   a.ev_join = c->ev_join;
   if (c->profiling) {
@@ -878,7 +913,8 @@ int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_
   a->ce = cnt + (size_t)mochi::kW2MsgArrays * m1;
   a->ce_cap = mochi::kW2MaxCertEntries * (uint32_t)m1;
   a->inl = (uint32_t*)(((uintptr_t)(a->ce + 11 * (size_t)a->ce_cap) + 15) & ~(uintptr_t)15);
-  a->cnt4 = a->inl + 4 * (size_t)mochi::kW2InlEntries * m1;
+  a->inl_ops = a->inl + 4 * (size_t)mochi::kW2InlEntries * m1;
+  a->cnt4 = a->inl_ops + 2 * (size_t)mochi::kW2InlOps * m1;  // 16-byte aligned: the two above are multiples of 4 words
   a->off4 = a->cnt4 + 4 * m1;
   a->status = status;
   a->scan_temp = c->w2_scan.p;
@@ -1019,6 +1055,7 @@ int mochi_verify_batch_device(mochi_ctx* c, const mochi_batch* b, const mochi_pa
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  new_call(c);
   rc = run_device(c, b, p, o, (hipStream_t)stream);  // NULL = the null stream, as in HIP
   (void)hipSetDevice(save);
   return rc;
@@ -1032,6 +1069,7 @@ int mochi_verify_batch(mochi_ctx* c, const mochi_batch* b, const mochi_params* p
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  new_call(c);
   rc = run_host_pipeline(c, b, p, o);
   (void)hipSetDevice(save);
   return rc;
@@ -1097,6 +1135,7 @@ int mochi_verify_write2_device(mochi_ctx* c, const mochi_write2_batch* w, const 
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
+  new_call(c);
   rc = run_write2_device(c, w, p, o, msg_status, (hipStream_t)stream);
   (void)hipSetDevice(save);
   return rc;
@@ -1288,8 +1327,7 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   }
   if (c->n_ids != c->n_keys) return fail(MOCHI_EINVAL, "server ids not set (mochi_ctx_set_server_ids)");
   std::lock_guard<std::mutex> lk(c->mu);
-  c->acc_dev = nullptr;
-  c->acc_words = 0;
+  new_call(c);
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);
@@ -1561,6 +1599,7 @@ int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const u
     if (signer[i] >= c->n_keys) return fail(MOCHI_EINVAL, "signer[%u] out of range", i);
   if (n == 0) return MOCHI_OK;
   std::lock_guard<std::mutex> lk(c->mu);
+  new_call(c);
   int save = 0;
   (void)hipGetDevice(&save);
   if (hipSetDevice(c->device) != hipSuccess) return fail(MOCHI_EHIP, "hipSetDevice(%d)", c->device);

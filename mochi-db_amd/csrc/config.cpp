@@ -7,7 +7,8 @@
 // Host only.  java.util.Properties.load text rules: logical lines joined on an
 // odd run of trailing backslashes, '#' / '!' comment lines, key ended by the
 // first unescaped '=', ':' or blank, \t \n \r \f \uXXXX escapes, last
-// duplicate wins.  StringUtils.split(s, ',') drops empty fields and trims
+// duplicate wins; the file is ISO-8859-1 and ids reach the wire as UTF-8
+// (Utf16ToUtf8 below).  StringUtils.split(s, ',') drops empty fields and trims
 // nothing; Integer.parseInt accepts an optional sign and decimal digits only.
 #include <cerrno>
 #include <cstdio>
@@ -39,8 +40,42 @@ int cfail(const std::string& msg) { return mochi::set_error(MOCHI_EINVAL, msg); 
 void put_utf8(std::string& s, uint32_t cp) {
   if (cp < 0x80) s += (char)cp;
   else if (cp < 0x800) s += (char)(0xC0 | cp >> 6), s += (char)(0x80 | (cp & 0x3F));
-  else s += (char)(0xE0 | cp >> 12), s += (char)(0x80 | ((cp >> 6) & 0x3F)), s += (char)(0x80 | (cp & 0x3F));
+  else if (cp < 0x10000)
+    s += (char)(0xE0 | cp >> 12), s += (char)(0x80 | ((cp >> 6) & 0x3F)), s += (char)(0x80 | (cp & 0x3F));
+  else
+    s += (char)(0xF0 | cp >> 18), s += (char)(0x80 | ((cp >> 12) & 0x3F)), s += (char)(0x80 | ((cp >> 6) & 0x3F)),
+        s += (char)(0x80 | (cp & 0x3F));
 }
+
+// The Java String a Properties value becomes, as the UTF-8 bytes protobuf-java
+// puts on the wire for it (CodedOutputStream.writeString): Properties.load(
+// InputStream) reads the file as ISO-8859-1, so every raw byte is one UTF-16
+// code unit (>= 0x80: a 2-byte UTF-8 sequence), a \uXXXX escape is one code
+// unit, a high + low surrogate pair is one supplementary code point, and an
+// unpaired surrogate becomes '?' (String.getBytes(UTF_8), protobuf's fallback
+// for strings Utf8.encode refuses).
+struct Utf16ToUtf8 {
+  std::string& o;
+  uint32_t hi = 0;  // pending high surrogate
+  void unit(uint32_t u) {
+    if (hi) {
+      if (u >= 0xDC00 && u <= 0xDFFF) {
+        put_utf8(o, 0x10000 + ((hi - 0xD800) << 10) + (u - 0xDC00));
+        hi = 0;
+        return;
+      }
+      o += '?';
+      hi = 0;
+    }
+    if (u >= 0xD800 && u <= 0xDBFF) hi = u;
+    else if (u >= 0xDC00 && u <= 0xDFFF) o += '?';
+    else put_utf8(o, u);
+  }
+  void end() {
+    if (hi) o += '?';
+    hi = 0;
+  }
+};
 
 bool is_blank(char c) { return c == ' ' || c == '\t' || c == '\f'; }
 
@@ -102,17 +137,17 @@ bool parse_properties(const char* text, size_t len, std::map<std::string, std::s
     std::string raw_val = line.substr(k);
     for (int part = 0; part < 2; part++) {
       const std::string& in = part ? raw_val : raw_key;
-      std::string& o = part ? val : key;
+      Utf16ToUtf8 o{part ? val : key};
       for (size_t x = 0; x < in.size(); x++) {
         if (in[x] != '\\' || x + 1 >= in.size()) {
-          o += in[x];
+          o.unit((uint8_t)in[x]);  // ISO-8859-1: byte = code unit
           continue;
         }
         const char c = in[++x];
-        if (c == 't') o += '\t';
-        else if (c == 'n') o += '\n';
-        else if (c == 'r') o += '\r';
-        else if (c == 'f') o += '\f';
+        if (c == 't') o.unit('\t');
+        else if (c == 'n') o.unit('\n');
+        else if (c == 'r') o.unit('\r');
+        else if (c == 'f') o.unit('\f');
         else if (c == 'u') {
           if (x + 4 >= in.size()) {
             err = "malformed \\uxxxx encoding";
@@ -131,9 +166,10 @@ bool parse_properties(const char* text, size_t len, std::map<std::string, std::s
             }
           }
           x += 4;
-          put_utf8(o, cp);
-        } else o += c;
+          o.unit(cp);
+        } else o.unit((uint8_t)c);
       }
+      o.end();
     }
     out[key] = val;
   }

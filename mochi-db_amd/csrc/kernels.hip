@@ -17,8 +17,8 @@
 
 #include "../../include/mochi_hip.h"
 #include "kernels.h"
+#include "prep_dev.h"
 #include "proto_dev.h"
-#include "sha256_dev.h"
 
 namespace mochi {
 
@@ -26,28 +26,9 @@ namespace mochi {
 // ---------------------------------------------------------------------------
 // k_grant_prep: parse + SHA-256, certificate order (lane = grant).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_grant_prep(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ goff,
-                                                    const uint32_t* __restrict__ glen, uint32_t n,
-                                                    uint32_t* __restrict__ digest /* [8][n] */,
-                                                    int64_t* __restrict__ ts_out, uint64_t* __restrict__ hash_off_out, uint32_t* __restrict__ hash_len_out,
-                                                    uint8_t* __restrict__ flags) {
+__global__ __launch_bounds__(256) void k_grant_prep(const PrepArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t* p = blob + goff[i];
-  const uint32_t l = glen[i];
-  ByteReader r;
-  r.init(p, l);
-  int64_t ts = 0;
-  uint32_t hoff = 0, hlen = 0;
-  const bool ok = parse_grant(r, ts, hoff, hlen);
-  uint32_t h[8];
-  sha256(p, l, h);
-#pragma unroll
-  for (int q = 0; q < 8; q++) digest[(size_t)q * n + i] = h[q];
-  ts_out[i] = ok ? ts : 0;
-  hash_off_out[i] = goff[i] + hoff;
-  hash_len_out[i] = ok ? hlen : 0xFFFFFFFFu;
-  flags[i] = ok ? MOCHI_GRANT_PARSED : 0;
+  if (i < a.n) grant_prep_one(a, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -475,12 +456,14 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   auto mark = [&](int stage, bool end, hipStream_t s) {
     if (a.prof_events) (void)hipEventRecord(a.prof_events[2 * stage + (end ? 1 : 0)], s);
   };
-  // grant prep (parse + SHA-256) only feeds k_rsa_final and k_tally, so it runs
-  // beside k_rsa_pow on the aux stream and fills its idle issue slots (it is
-  // latency-bound); the launch stream joins it before k_rsa_final.  It forks
-  // AFTER bucketing: run beside prep, the short bucket kernels (which gate
-  // k_rsa_pow) took ~4x longer
-  const bool prep = N && !a.skip_prep_tally;
+  // grant prep (parse + SHA-256) only feeds k_rsa_final and k_tally.  By
+  // default k_rsa_pow does it in the half-phases its SIMD-partner schedule
+  // leaves idle (rsa_pow.hip); with a.prep_kernel it is k_grant_prep, beside
+  // k_rsa_pow on the aux stream (joined before k_rsa_final) or, without aux,
+  // serialised.  That fork comes AFTER bucketing: run beside prep, the short
+  // bucket kernels (which gate k_rsa_pow) took ~4x longer
+  PrepArgs pa{a.blob, a.grant_off, a.grant_len, N, a.digest, a.ts, a.hash_off, a.hash_len, a.flags};
+  const bool prep = N && !a.skip_prep_tally && a.prep_kernel;
   const bool fork = prep && a.aux;
   hipStream_t ps = fork ? a.aux : st;
   mark(kStageBucket, false, st);
@@ -504,15 +487,15 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   }
   mark(kStagePrep, false, ps);
   if (prep)
-    hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, a.blob, a.grant_off, a.grant_len, N,
-                       a.digest, a.ts, a.hash_off, a.hash_len, a.flags);
+    hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
   mark(kStagePrep, true, ps);
   if (fork) {
     hipError_t e = hipEventRecord(a.ev_join, a.aux);
     if (e != hipSuccess) return e;
   }
   mark(kStagePow, false, st);
-  if (N) launch_rsa_pow(a, st);
+  if (!(N && !a.skip_prep_tally && !a.prep_kernel)) pa.n = 0;  // prep fused into k_rsa_pow?
+  if (N) launch_rsa_pow(a, pa, st);
   mark(kStagePow, true, st);
   if (fork) {
     hipError_t e = hipStreamWaitEvent(st, a.ev_join, 0);

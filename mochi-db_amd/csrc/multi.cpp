@@ -29,7 +29,8 @@
 namespace mochi {
 int set_error(int code, const std::string& msg);  // capi.cpp: the text mochi_last_error() returns
 // capi.cpp: the accept bitmap of the context's last host-path call, on its device
-const uint32_t* ctx_last_accept_dev(mochi_ctx* c, uint32_t* words, int* device, hipStream_t* stream);
+uint64_t ctx_call_gen();  // capi.cpp: generation of this thread's last context call
+int ctx_copy_accept_dev(mochi_ctx* c, uint64_t gen, int device, uint32_t* dst, uint32_t need, hipStream_t st);
 }
 
 namespace {
@@ -306,7 +307,7 @@ void slice_batch(const mochi_batch* B, uint32_t c0, uint32_t c1, SubBatch& s) {
 // the final verdict (messages decided by the host fallback decoder) uploads its
 // host bits into its slot instead.
 int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::vector<std::vector<uint32_t>>& shard_bits,
-                uint32_t* bits_out) {
+                const std::vector<uint64_t>& gen, uint32_t* bits_out) {
   const int n = (int)m->devices.size();
   const uint32_t W = mochi_shard_words((uint32_t)n, cert_lo.data());
   std::vector<int> rc(n, MOCHI_OK);
@@ -328,15 +329,14 @@ int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::
     }
     uint32_t* slot = m->gathered[i] + (size_t)W * i;
     const uint32_t need = words(cert_lo[i + 1] - cert_lo[i]);  // <= W
-    uint32_t dev_words = 0;
-    int dev = -1;
-    hipStream_t cst = nullptr;
-    const uint32_t* d = mochi::ctx_last_accept_dev(m->ctx[i], &dev_words, &dev, &cst);
     hipError_t e = hipMemsetAsync(slot, 0, 4 * (size_t)W, m->stream[i]);
     if (e == hipSuccess && need) {
-      if (d && dev == m->devices[i] && dev_words >= need)
-        e = hipMemcpyAsync(slot, d, 4 * (size_t)need, hipMemcpyDeviceToDevice, m->stream[i]);
-      else {
+      // the shard's bitmap where its verify left it, if no later call on the
+      // context has touched its buffers since (checked and copied under the
+      // context's lock); otherwise the host bits the verify returned
+      const int d = mochi::ctx_copy_accept_dev(m->ctx[i], gen[i], m->devices[i], slot, need, m->stream[i]);
+      if (d == MOCHI_EHIP) e = hipErrorUnknown;
+      else if (d != MOCHI_OK) {
         const size_t have = shard_bits[i].size() < need ? shard_bits[i].size() : need;
         e = hipMemcpyAsync(slot, shard_bits[i].data(), 4 * have, hipMemcpyHostToDevice, m->stream[i]);
       }
@@ -372,6 +372,7 @@ int mochi_mverify_batch(mochi_mctx* m, const mochi_batch* b, const mochi_params*
   std::vector<uint32_t> lo(n + 1);
   mochi_shard_plan(b->n_certs, b->cert_grant_off, (uint32_t)n, lo.data());
   std::vector<std::vector<uint32_t>> bits(n);
+  std::vector<uint64_t> gen(n, 0);
   std::vector<int> rc(n, MOCHI_OK);
   std::vector<std::string> err(n);
   auto work = [&](int i) {
@@ -390,6 +391,7 @@ int mochi_mverify_batch(mochi_mctx* m, const mochi_batch* b, const mochi_params*
     v.op_g0 = o->op_g0 ? o->op_g0 + o0 : nullptr;
     v.op_ts = o->op_ts ? o->op_ts + o0 : nullptr;
     rc[i] = mochi_verify_batch(m->ctx[i], &s.b, p, &v);
+    gen[i] = mochi::ctx_call_gen();
     if (rc[i]) err[i] = mochi_last_error();
   };
   std::vector<std::thread> th;
@@ -397,7 +399,7 @@ int mochi_mverify_batch(mochi_mctx* m, const mochi_batch* b, const mochi_params*
   for (auto& t : th) t.join();
   for (int i = 0; i < n; i++)
     if (rc[i]) return mfail(rc[i], "device " + std::to_string(m->devices[i]) + ": " + err[i]);
-  return b->n_certs ? gather_bits(m, lo, bits, o->cert_accept_bits) : MOCHI_OK;
+  return b->n_certs ? gather_bits(m, lo, bits, gen, o->cert_accept_bits) : MOCHI_OK;
 }
 
 int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* w, const mochi_params* p, mochi_verdicts* o,
@@ -415,6 +417,7 @@ int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* w, const mochi
   std::vector<uint32_t> lo(n + 1);
   mochi_shard_plan(w->n_msgs, prefix.data(), (uint32_t)n, lo.data());
   std::vector<std::vector<uint32_t>> bits(n);
+  std::vector<uint64_t> gen(n, 0);
   std::vector<int> rc(n, MOCHI_OK);
   std::vector<std::string> err(n);
   auto work = [&](int i) {
@@ -444,6 +447,7 @@ int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* w, const mochi
     v.op_g0 = o->op_g0 ? o->op_g0 + o0 : nullptr;
     v.op_ts = o->op_ts ? o->op_ts + o0 : nullptr;
     rc[i] = mochi_verify_write2(m->ctx[i], &s, p, &v, msg_status ? msg_status + m0 : nullptr);
+    gen[i] = mochi::ctx_call_gen();
     if (rc[i]) err[i] = mochi_last_error();
   };
   std::vector<std::thread> th;
@@ -451,7 +455,7 @@ int mochi_mverify_write2(mochi_mctx* m, const mochi_write2_batch* w, const mochi
   for (auto& t : th) t.join();
   for (int i = 0; i < n; i++)
     if (rc[i]) return mfail(rc[i], "device " + std::to_string(m->devices[i]) + ": " + err[i]);
-  return w->n_msgs ? gather_bits(m, lo, bits, o->cert_accept_bits) : MOCHI_OK;
+  return w->n_msgs ? gather_bits(m, lo, bits, gen, o->cert_accept_bits) : MOCHI_OK;
 }
 
 int mochi_mctx_gathered_bits(mochi_mctx* m, int i, const uint32_t** d_bits, uint32_t* words_per_device) {

@@ -50,6 +50,19 @@ constexpr int kMaxGroupDepth = 16;    // register-resident group stack of the fa
 constexpr int kDeepGroupDepth = 100;  // CodedInputStream's default recursion limit (protobuf-java)
 
 __device__ __forceinline__ bool rd_varint(ByteReader& r, uint32_t& pos, uint64_t& v) {
+  if (pos + 1 < r.len) {  // one- and two-byte varints (tags, lengths) without the loop
+    const uint32_t c0 = r.at(pos), c1 = r.at(pos + 1);
+    if (c0 < 0x80u) {
+      v = c0;
+      pos += 1;
+      return true;
+    }
+    if (c1 < 0x80u) {
+      v = (c0 & 0x7Fu) | (c1 << 7);
+      pos += 2;
+      return true;
+    }
+  }
   uint64_t x = 0;
 #pragma unroll 1
   for (int i = 0; i < 10; i++) {
@@ -155,20 +168,39 @@ __device__ __forceinline__ bool rd_string(ByteReader& r, uint32_t& pos, uint32_t
 // kDepth = size of the unknown-group stack.  The fast instance keeps 16 entries
 // in registers and reports a deeper nesting through `too_deep`; parse_grant
 // then re-parses with the 100-deep instance, kept out of line (scratch stack).
-template <int kDepth>
+// bytes of the minimal varint encoding of v
+__device__ __forceinline__ uint32_t varint_size(uint64_t v) {
+  const uint32_t bits = v ? 64u - (uint32_t)__builtin_clzll(v) : 1u;
+  return (bits + 6) / 7;
+}
+
+// CANON (the wire decoder): also report in `canon` whether the bytes are
+// exactly Grant.toByteArray() of the Grant they parse to
+// (MochiProtocol.java:7556-7574): fields 1..5 in order, each at most once,
+// none at its default, one-byte tags, minimal varints and lengths, no unknown
+// fields, status an int32 (writeEnum sign-extends) -- decided during the parse
+// instead of a second walk.
+template <int kDepth, bool CANON = false>
 __device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
-                                     uint32_t& oid_off, uint32_t& oid_len, bool& too_deep) {
+                                     uint32_t& oid_off, uint32_t& oid_len, bool& too_deep, bool* canon = nullptr) {
   uint32_t pos = 0;
   int64_t t = 0;
   uint32_t hoff = 0, hlen = 0, ooff = 0, olen = 0;
   uint32_t stack[kDepth];
   int depth = 0;
+  uint32_t last_field = 0;
+  bool cn = true;
 #pragma unroll 1
   while (pos < r.len) {
     uint64_t tag64;
+    const uint32_t p0 = pos;
     if (!rd_varint(r, pos, tag64)) return false;
     const uint32_t tag = (uint32_t)tag64, field = tag >> 3, wt = tag & 7;
     if (field == 0) return false;
+    if (CANON) {
+      cn = cn && pos - p0 == 1 && field > last_field && depth == 0;
+      last_field = field;
+    }
     if (depth > 0) {
       if (wt == 4) {
         if (stack[depth - 1] != field) return false;
@@ -177,20 +209,28 @@ __device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_
       }
     } else {
       if (tag == 10) {
+        const uint32_t p1 = pos;
         if (!rd_string(r, pos, ooff, olen)) return false;
+        if (CANON) cn = cn && olen != 0 && ooff - p1 == varint_size(olen);
         continue;
       }
       if (tag == 16 || tag == 24 || tag == 40) {
         uint64_t v;
+        const uint32_t p1 = pos;
         if (!rd_varint(r, pos, v)) return false;
         if (tag == 16) t = (int64_t)v;
+        if (CANON)
+          cn = cn && v != 0 && pos - p1 == varint_size(v) && (tag != 40 || (int64_t)v == (int64_t)(int32_t)(uint32_t)v);
         continue;
       }
       if (tag == 34) {
+        const uint32_t p1 = pos;
         if (!rd_string(r, pos, hoff, hlen)) return false;
+        if (CANON) cn = cn && hlen != 0 && hoff - p1 == varint_size(hlen);
         continue;
       }
     }
+    if (CANON) cn = false;  // an unknown field, a known one with a foreign wire type, or a group
     switch (wt) {
       case 0: {
         uint64_t v;
@@ -230,6 +270,7 @@ __device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_
   hash_len = hlen;
   oid_off = ooff;
   oid_len = olen;
+  if (CANON) *canon = cn;
   return true;
 }
 
@@ -265,6 +306,19 @@ __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_of
   oid_off = f.oid_off;
   oid_len = f.oid_len;
   return f.ok != 0;
+}
+
+// parse validity (as parse_grant) + canonical encoding (parse_grant_t CANON).
+// A grant that needs the deep parser has a group in it: parsed, never canonical.
+__device__ inline bool parse_grant_canon(ByteReader& r, bool& canon) {
+  int64_t ts;
+  uint32_t ho, hl, oo, ol;
+  bool too_deep = false;
+  canon = false;
+  if (parse_grant_t<kMaxGroupDepth, true>(r, ts, ho, hl, oo, ol, too_deep, &canon)) return true;
+  canon = false;
+  if (!too_deep) return false;
+  return parse_grant_deep(r.base, r.len).ok != 0;
 }
 
 __device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {

@@ -22,7 +22,22 @@
 // Group = 512 slots of ONE signer (buckets are 512-aligned), block = 8 waves
 // = one group at a time; the signer's 100 KB image is staged in LDS; 2 waves
 // per SIMD; persistent blocks, one per CU.
+//
+// SIMD partners in opposite phases.  Waves w and w + 4 share a SIMD.  A
+// squaring is two phases of very different shape -- x^2 is VALU issue (2,109
+// 64-bit mads + glue), the fold is the matrix pipe (200 MFMAs x 32 cycles) plus
+// a short assembly -- and left free-running the partners' phases fall where
+// they may: both in x^2 (VALU saturated, matrix pipe idle) or both in the fold
+// (the reverse) much of the time.  So waves 4-7 run one phase behind waves 0-3
+// and a block barrier ends every phase: one wave's x^2 always runs beside its
+// partner's fold, whose MFMAs (at s_setprio 1, so they issue the moment they
+// are ready) co-execute with the x^2's VALU.  Per group each half has one phase
+// with nothing to square (waves 4-7 the first, waves 0-3 the last); those
+// half-phases do the group's GRANT PREP (parse + SHA-256 of 512 grants in
+// certificate order, prep_dev.h) instead of a separate kernel, which the
+// matrix-core kernel, holding every VGPR of the CU, would never let co-reside.
 #include "fold_dev.h"
+#include "prep_dev.h"
 #include "rsa_common.h"
 
 // MOCHI_POW_STAMPS (measurement builds only, `make ab`): per wave, s_memtime
@@ -39,7 +54,7 @@ __device__ unsigned long long g_pow_stamps[4096][5];
 namespace {
 
 struct Stamps {
-  uint64_t x2 = 0, fold = 0, n = 0, mid = 0;
+  uint64_t x2 = 0, fold = 0, n = 0, prep = 0;
 };
 
 __device__ __forceinline__ uint64_t stamp() {
@@ -53,65 +68,118 @@ __device__ __forceinline__ uint64_t stamp() {
 #endif
 }
 
-__device__ __forceinline__ void fold_sqr(uint32_t (&x)[kL], const v4i* __restrict__ wl, cptr cadd, Stamps& st) {
-  uint32_t t[2 * kL];
-  const uint64_t t0 = stamp();
-#if MOCHI_POW_STAMPS
-  {  // kara_square with a stamp after the middle product (M's one chain vs L and H in lockstep)
-    uint32_t sx[kKH];
-#pragma unroll
-    for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
-    kara_middle(t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(sx, carry); });
-  }
-  st.mid += stamp() - t0;
-  kara_combine(
-      t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(x, carry); },
-      [&](auto kc, uint64_t& carry) { return square_col<kKH, decltype(kc)::value>(x, carry); });
-#else
-  kara_square(x, t);  // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
-#endif
-  const uint64_t t1 = stamp();
-  fold_reduce<false, true>(t, x, wl, cadd, nullptr);
-  const uint64_t t2 = stamp();
-  st.x2 += t1 - t0;
-  st.fold += t2 - t1;
-  st.n++;
+__device__ __forceinline__ void phase_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
 }
 
+struct PowArgs {
+  const uint32_t* perm;
+  uint32_t n_slots;
+  const uint8_t* sig;
+  const uint16_t* signer;
+  const FoldKey* fold;
+  uint32_t* zout;
+};
+
 // Persistent: one block per CU walks a contiguous range of 512-slot groups, so
-// the CU never idles between blocks (a block's 8 waves would otherwise all wait
-// for its slowest before the next block could take the LDS) and the signer's
-// image is staged only when the key changes along the range (block-uniform).
-__global__ __launch_bounds__(512, 1) void k_rsa_pow(const uint32_t* __restrict__ perm, uint32_t n_slots,
-                                                    const uint8_t* __restrict__ sig,
-                                                    const uint16_t* __restrict__ signer,
-                                                    const FoldKey* __restrict__ fold, uint32_t* __restrict__ zout) {
+// the CU never idles between blocks and the signer's image is staged only when
+// the key changes along the range (block-uniform).  The block also owns a
+// contiguous range of grants to prep, 512 per group iteration (the ranges are
+// proportional splits of n_slots >= N and of N, so at most one chunk is left
+// for the tail loop).
+__global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a, const PrepArgs pa) {
   __shared__ v4i w[kFoldImgBytes / 16];
   Stamps st;
   const uint64_t t_begin = stamp();
-  for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
+  // waves 4-7 run one phase behind.  Read through readfirstlane so the compiler
+  // KNOWS it is wave-uniform: the barriers below sit under `if (lag)`, and a
+  // barrier under a branch it takes for divergent is exec-masked code, into
+  // whose join it once hoisted a VALU constant that the masked-off waves never
+  // wrote (half the signatures wrong)
+  const bool lag = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
+  const uint32_t n_groups = (a.n_slots + kBucketAlign - 1) / kBucketAlign;
+  const uint32_t g_begin = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
+  const uint32_t g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
+  const uint32_t p_begin = (uint32_t)((uint64_t)blockIdx.x * pa.n / gridDim.x);
+  const uint32_t p_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * pa.n / gridDim.x);
+  // this wave's 64 grants of iteration j's chunk
+  auto prep_chunk = [&](uint32_t j) {
+    const uint64_t t0 = stamp();
+    const uint64_t i = (uint64_t)p_begin + (uint64_t)kBucketAlign * j + threadIdx.x;
+    if (i < p_end) grant_prep_one(pa, (uint32_t)i);
+    st.prep += stamp() - t0;
+  };
+  uint32_t cur_key = 0xFFFFFFFFu;
+  for (uint32_t grp = g_begin; grp < g_end; grp++) {
+    const uint32_t j = grp - g_begin;
+    const uint32_t base = grp * kBucketAlign;
+    // buckets are 512-aligned and padded only at their tail: a group whose
+    // first slot is empty is all padding (every thread reads the same slot)
+    const uint32_t g_lead = __builtin_amdgcn_readfirstlane(a.perm[base]);
+    if (g_lead == 0xFFFFFFFFu) {
+      prep_chunk(j);
+      continue;
+    }
+    const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)a.signer[g_lead]);
+    if (key != cur_key) {
+      __syncthreads();  // the old image is no longer read
+      const v4i* src = (const v4i*)a.fold[key].img;
+      for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
+      __syncthreads();
+      cur_key = key;
+    }
     const uint32_t slot = base + threadIdx.x;
-    const uint32_t g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
+    const uint32_t g = slot < a.n_slots ? a.perm[slot] : 0xFFFFFFFFu;
     const bool active = g != 0xFFFFFFFFu;
-    if (__ballot(active) == 0) return;  // this wave's quarter of the group is padding
+    if (__ballot(active) == 0) {  // this wave's quarter of the group is padding: prep, keep the barrier count
+      prep_chunk(j);
+#pragma unroll 1
+      for (int i = 0; i < 33; i++) phase_barrier();
+      continue;
+    }
+    if (lag) {  // phase 0: the partner squares, this wave preps
+      prep_chunk(j);
+      phase_barrier();
+    }
     uint32_t x[kL];
     {
       uint32_t wd[64];
-      load_sig_words(sig, active ? g : g_lead, wd);  // inactive lanes shadow the lead grant (never stored)
+      load_sig_words(a.sig, active ? g : g_lead, wd);  // inactive lanes shadow the lead grant (never stored)
       words_to_limbs(wd, x);
     }
-    const cptr c = as_const(fold[key].cadd);
+    const cptr c = as_const(a.fold[key].cadd);
 #pragma unroll 1
     for (int it = 0; it < 16; it++) {
       cptr ci = c;
       asm volatile("" : "+s"(ci));  // keep the 74 cadd loads inside the loop (SGPR pressure if hoisted)
-      fold_sqr(x, w + (threadIdx.x & 63), ci, st);
+      uint32_t t[2 * kL];
+      const uint64_t t0 = stamp();
+      kara_square(x, t);  // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
+      const uint64_t t1 = stamp();
+      phase_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      const uint64_t t2 = stamp();
+      fold_reduce<false, true>(t, x, w + (threadIdx.x & 63), ci, nullptr);
+      const uint64_t t3 = stamp();
+      __builtin_amdgcn_s_setprio(0);
+      phase_barrier();
+      st.x2 += t1 - t0;
+      st.fold += t3 - t2;
+      st.n++;
     }
     if (active) {
 #pragma unroll
-      for (int j = 0; j < kL; j++) zout[(size_t)j * n_slots + slot] = x[j];
+      for (int q = 0; q < kL; q++) a.zout[(size_t)q * a.n_slots + slot] = x[q];
     }
-  });
+    if (!lag) {  // phase 32: the partner folds its last squaring, this wave preps
+      prep_chunk(j);
+      phase_barrier();
+    }
+  }
+  // chunks beyond the group range (no squaring left to pair with)
+  for (uint32_t j = g_end - g_begin; (uint64_t)p_begin + (uint64_t)kBucketAlign * j < p_end; j++) prep_chunk(j);
 #if MOCHI_POW_STAMPS
   const uint64_t t_end = stamp();
   const uint32_t wv = blockIdx.x * 8 + (threadIdx.x >> 6);
@@ -120,7 +188,7 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const uint32_t* __restrict__
     g_pow_stamps[wv][1] = st.fold;
     g_pow_stamps[wv][2] = t_end - t_begin;
     g_pow_stamps[wv][3] = st.n;
-    g_pow_stamps[wv][4] = st.mid;
+    g_pow_stamps[wv][4] = st.prep;
   }
 #else
   (void)t_begin;
@@ -136,11 +204,10 @@ extern "C" int mochi_debug_pow_stamps(unsigned long long* out, unsigned n_waves)
 }
 #endif
 
-void launch_rsa_pow(const LaunchArgs& a, hipStream_t st) {
+void launch_rsa_pow(const LaunchArgs& a, const PrepArgs& prep, hipStream_t st) {
   const uint32_t blocks = fold_grid(a.n_slots);
-  if (blocks)
-    hipLaunchKernelGGL(k_rsa_pow, dim3(blocks), dim3(kBucketAlign), 0, st, a.perm, a.n_slots, a.sig, a.signer, a.fold,
-                       a.xbuf);
+  const PowArgs pw{a.perm, a.n_slots, a.sig, a.signer, a.fold, a.xbuf};
+  if (blocks) hipLaunchKernelGGL(k_rsa_pow, dim3(blocks), dim3(kBucketAlign), 0, st, pw, prep);
 }
 
 }  // namespace mochi

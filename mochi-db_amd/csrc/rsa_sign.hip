@@ -42,10 +42,26 @@ namespace {
 // multiply by T[window] -- including window 0, so the operation sequence
 // depends only on the exponent's length, not on its bits.  ~1,020 squarings +
 // 255 multiplies + 16 table products per 1024-bit half, vs ~1,023 + ~512 for
-// square-and-multiply.  The window value is wave-uniform (one key per
-// launch), so T lives in per-lane private (scratch) memory indexed by a
-// uniform value: 37 coalesced scratch loads per multiply; the runtime sizes
-// scratch for the resident waves only.
+// square-and-multiply.  T lives in per-lane private (scratch) memory.  The
+// window value is a digit of the SECRET exponent, so T is never indexed by it:
+// every multiply reads all 16 entries in a fixed order and keeps one with a
+// mask computed in VGPRs (v_cmp / v_cndmask, no branch on the digit), so the
+// addresses, the instruction stream and its timing are the same for every
+// digit (16 x 37 scratch loads per multiply, ~5 % of the signing time).
+template <int L>
+__device__ __forceinline__ void table_select(uint32_t (&out)[L], const uint32_t (&tbl)[16][L], uint32_t w) {
+  uint32_t wv = w;
+  asm volatile("" : "+v"(wv));  // the digit as a per-lane value: compares stay vector, never a scalar branch
+#pragma unroll
+  for (int j = 0; j < L; j++) out[j] = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < 16; v++) {
+    const uint32_t m = 0u - (uint32_t)(wv == v);
+#pragma unroll
+    for (int j = 0; j < L; j++) out[j] |= tbl[v][j] & m;
+  }
+}
+
 template <int L>
 __device__ __forceinline__ void mont_pow(uint32_t (&acc)[L], const uint32_t (&base)[L], cptr r3, cptr e,
                                          uint32_t ebits, cptr n, uint32_t n0inv) {
@@ -74,15 +90,12 @@ __device__ __forceinline__ void mont_pow(uint32_t (&acc)[L], const uint32_t (&ba
   const int nwin = (int)(ebits + 3) >> 2;  // ebits >= 2
   auto window = [&](int i) -> uint32_t { return (e[i >> 3] >> ((i & 7) * 4)) & 15u; };
   const uint32_t top = window(nwin - 1);  // != 0: the exponent's top bit lies in it
-#pragma unroll
-  for (int j = 0; j < L; j++) acc[j] = tbl[top][j];
+  table_select<L>(acc, tbl, top);
 #pragma unroll 1
   for (int i = nwin - 2; i >= 0; i--) {
 #pragma unroll 1
     for (int s = 0; s < 4; s++) mont_sqr_n<L>(acc, n, n0inv);
-    const uint32_t w = window(i);
-#pragma unroll
-    for (int j = 0; j < L; j++) t[j] = tbl[w][j];
+    table_select<L>(t, tbl, window(i));
     mont_mul_n<L, false>(acc, acc, nullptr, t, n, n0inv);
   }
 }

@@ -31,6 +31,7 @@ struct W2Args {
   uint32_t* ce;
   uint32_t ce_cap;
   uint32_t* inl;  // [M+1][kW2InlEntries][4], 16-byte aligned: level 1's first entries (key / value slices)
+  uint32_t* inl_ops;  // [M+1][kW2InlOps][2]: level 1's first operations' operand1 slices (key slot lookup)
   uint32_t* cnt4;  // [M+1][4], 16-byte aligned: decoded grants, ops, MultiGrants per message (one scan)
   uint32_t* off4;  // [M+1][4]: their exclusive scan (unpacked into cert_*_off by k_w2_ops)
   uint8_t* status;  // [M]
@@ -62,9 +63,13 @@ constexpr int kW2MsgArrays = 13;
 // Level 1 records the key / value slices of a message's first kW2InlEntries
 // certificate entries, so the compact entry list is copied, not re-parsed.
 constexpr uint32_t kW2InlEntries = 4;
+// ... and the operand1 (key) slices of its first kW2InlOps operations, so level
+// 2's key-slot lookup compares keys instead of re-walking the transaction.
+constexpr uint32_t kW2InlOps = 4;
 inline size_t w2_scratch_words(uint32_t M) {
   return (size_t)kW2MsgArrays * ((size_t)M + 1) + 11 * (size_t)kW2MaxCertEntries * ((size_t)M + 1) +
-         4 * (size_t)kW2InlEntries * ((size_t)M + 1) + 8 * ((size_t)M + 1) + 4;  // + 4: 16-byte alignment
+         4 * (size_t)kW2InlEntries * ((size_t)M + 1) + 2 * (size_t)kW2InlOps * ((size_t)M + 1) + 8 * ((size_t)M + 1) +
+         4;  // + 4: 16-byte alignment
 }
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
 hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans

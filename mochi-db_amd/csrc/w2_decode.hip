@@ -51,6 +51,21 @@ struct Fld {
 };
 
 __device__ __forceinline__ bool vint(ByteReader& r, uint32_t& pos, uint32_t end, uint64_t& v) {
+  // one- and two-byte varints (every tag, and every length below 16 KiB) without
+  // the loop: most lanes of a wave take this branch together
+  if (pos + 1 < end) {
+    const uint32_t c0 = r.at(pos), c1 = r.at(pos + 1);
+    if (c0 < 0x80u) {
+      v = c0;
+      pos += 1;
+      return true;
+    }
+    if (c1 < 0x80u) {
+      v = (c0 & 0x7Fu) | (c1 << 7);
+      pos += 2;
+      return true;
+    }
+  }
   uint64_t x = 0;
 #pragma unroll 1
   for (int i = 0; i < 10; i++) {
@@ -168,24 +183,24 @@ __device__ int next_fld(ByteReader& r, uint32_t& pos, uint32_t end, Fld& f) {
 }
 
 // ---- validity: what protobuf-java's parser checks ---------------------------
-__device__ bool valid_grant_at(ByteReader& r, uint32_t off, uint32_t len) {
+__device__ bool valid_grant_at(ByteReader& r, uint32_t off, uint32_t len, bool& canon) {
   ByteReader g;
   g.init(r.base + off, len);
-  int64_t ts;
-  uint32_t ho, hl;
-  return parse_grant(g, ts, ho, hl);
+  return parse_grant_canon(g, canon);
 }
 
 struct Entry {
   uint32_t koff, klen;  // key (last occurrence; default "")
   uint32_t voff, vlen;  // value (last occurrence; default empty)
   uint32_t nval;
+  bool canon;           // Grant value (kind 1): the last value is canonical Grant bytes
 };
 
 // map<string, V> entry; kind 0 = bytes value, 1 = Grant value: validated, and
 // its key and value read as read_entry reads them (last occurrence of each)
 __device__ bool valid_leaf_read(ByteReader& r, uint32_t off, uint32_t len, int kind, Entry& e) {
   e.koff = e.klen = e.voff = e.vlen = e.nval = 0;
+  e.canon = false;
   uint32_t pos = off, end = off + len;
   Fld f;
   int rc;
@@ -197,12 +212,15 @@ __device__ bool valid_leaf_read(ByteReader& r, uint32_t off, uint32_t len, int k
       e.koff = f.off;
       e.klen = f.len;
     } else if (f.field == 2) {
-      if (kind == 1 && !valid_grant_at(r, f.off, f.len)) return false;
+      if (kind == 1 && !valid_grant_at(r, f.off, f.len, e.canon)) return false;
       e.voff = f.off;
       e.vlen = f.len;
       e.nval++;
     }
   }
+  // an entry without a value holds the default Grant, whose toByteArray() is
+  // empty: canonical, as a zero-length value is
+  if (kind == 1 && e.nval == 0) e.canon = true;
   return rc == 0;
 }
 
@@ -250,14 +268,27 @@ __device__ bool all_ld(ByteReader& r, uint32_t off, uint32_t len, uint32_t field
   return rc == 0;
 }
 
-__device__ bool valid_operation(ByteReader& r, uint32_t off, uint32_t len) {
+// (ko, kl): the operation's operand1 as last_string(.., 2, ..) reads it
+__device__ bool valid_operation(ByteReader& r, uint32_t off, uint32_t len, uint32_t& ko, uint32_t& kl) {
   uint32_t pos = off, end = off + len;
   Fld f;
   int rc;
+  ko = kl = 0;
 #pragma unroll 1
   while ((rc = next_fld(r, pos, end, f)) > 0)
-    if (f.wt == 2 && f.field >= 2 && f.field <= 4 && !valid_utf8(r, f.off, f.len)) return false;
+    if (f.wt == 2 && f.field >= 2 && f.field <= 4) {
+      if (!valid_utf8(r, f.off, f.len)) return false;
+      if (f.field == 2) {
+        ko = f.off;
+        kl = f.len;
+      }
+    }
   return rc == 0;
+}
+
+__device__ __forceinline__ bool valid_operation(ByteReader& r, uint32_t off, uint32_t len) {
+  uint32_t ko, kl;
+  return valid_operation(r, off, len, ko, kl);
 }
 
 __device__ bool valid_write2(ByteReader& r) {
@@ -456,6 +487,7 @@ struct W2Out {
 struct W2Msg {
   uint32_t *cnt_ce, *ce_base, *st_bits, *wc_off, *wc_len, *tx_off, *tx_len, *cnt_o;
   uint32_t* inl;  // [M][kW2InlEntries][4]: koff, klen, voff, vlen of the first entries
+  uint32_t* inl_ops;  // [M][kW2InlOps][2]: operand1 off, len of the first operations
 };
 
 // ---- level by level ------------------------------------------------------------
@@ -486,7 +518,8 @@ __device__ __noinline__ bool valid_write2_whole(const uint8_t* base, uint32_t le
 // Level 1 for one message; returns status bits.  nce = certificate entries,
 // nops = operations (both 0 when the message left the fast path).
 __device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint32_t& wc_off, uint32_t& wc_len,
-                              uint32_t& tx_off, uint32_t& tx_len, uint32_t* __restrict__ inl) {
+                              uint32_t& tx_off, uint32_t& tx_len, uint32_t* __restrict__ inl,
+                              uint32_t* __restrict__ inl_ops) {
   uint32_t n_wc = 0, n_tx = 0;
   bool whole = false;
   nce = nops = 0;
@@ -556,7 +589,9 @@ __device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint
           whole = true;
           break;
         }
-        if (!valid_operation(r, g.off, g.len)) return kStMal;
+        uint32_t ko, kl;
+        if (!valid_operation(r, g.off, g.len, ko, kl)) return kStMal;
+        if (nops <= kW2InlOps) ((uint2*)inl_ops)[nops - 1] = make_uint2(ko, kl);
       }
       if (!whole && rc2 < 0) return kStMal;
     }
@@ -651,6 +686,38 @@ __device__ __forceinline__ uint16_t find_signer(ByteReader& r, uint32_t so, uint
                                                 const IdTab* tab = nullptr) {
   const uint32_t tail = sl >= 4 ? ld4(r.base, so + sl - 4) : 0u;
   const bool fast = tab && sl >= 4 && sl <= 4 * kIdFast;
+  if (fast && n_ids <= kIdTab) {
+    // Usually exactly one staged id has this length and last word (server ids
+    // end in distinct UUIDs): pick it first, then compare it in full ONCE.  A
+    // loop that compares inside the candidate test runs that compare once per
+    // distinct candidate among the wave's lanes (R times at R servers).
+    uint32_t cand = ~0u, nc = 0;
+    bool unstaged = false;
+#pragma unroll 1
+    for (uint32_t k = 0; k < n_ids; k++) {
+      if (tab->len[k] != sl || tab->tail[k] != tail) continue;
+      if (tab->pos[k] == ~0u) unstaged = true;
+      if (nc++ == 0) cand = k;
+    }
+    if (nc == 0) return 0xFFFF;
+    if (nc == 1 && !unstaged) {
+      // the serverId's words from the aligned words that hold its bytes
+      const uintptr_t a = (uintptr_t)(r.base + so);
+      const uint32_t* wp = (const uint32_t*)(a & ~(uintptr_t)3);
+      const uint32_t sh = 8 * (uint32_t)(a & 3);
+      const uint32_t nw = (uint32_t)(((a & 3) + sl + 3) >> 2);  // aligned words holding a byte of it
+      const uint32_t* w = tab->w + tab->pos[cand];
+      uint32_t diff = 0, lo = wp[0];
+#pragma unroll
+      for (uint32_t t = 0; t < kIdFast; t++) {
+        if (4 * t + 4 > sl) break;
+        const uint32_t hi = t + 1 < nw ? wp[t + 1] : 0u;
+        diff |= (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) ^ w[t];
+        lo = hi;
+      }
+      return diff == 0 ? (uint16_t)cand : (uint16_t)0xFFFF;  // the tail matched already
+    }
+  }
 #pragma unroll 1
   for (uint32_t k = 0; k < n_ids; k++) {
     if (tab && k < kIdTab) {
@@ -688,6 +755,21 @@ __device__ __forceinline__ uint8_t find_key_slot(ByteReader& r, uint32_t tx_off,
     last_string(r, f.off, f.len, 2, oo, ol);
     if (key_eq(r, oo, ol, ko, kl)) return (uint8_t)j;
     j++;
+  }
+  return 0xFF;
+}
+
+// find_key_slot from level 1's record of the message's first kW2InlOps
+// operations (cnt_o[m] = operations on the wire; more than recorded: the walk)
+__device__ __forceinline__ uint8_t find_key_slot_rec(ByteReader& r, const W2Msg& s, uint32_t m, uint32_t ko,
+                                                     uint32_t kl) {
+  const uint32_t nops = s.cnt_o[m];
+  if (nops > kW2InlOps) return find_key_slot(r, s.tx_off[m], s.tx_len[m], ko, kl);
+  const uint2* q = (const uint2*)(s.inl_ops + (size_t)2 * kW2InlOps * m);
+#pragma unroll 1
+  for (uint32_t j = 0; j < nops; j++) {
+    const uint2 o = q[j];
+    if (key_eq(r, o.x, o.y, ko, kl)) return (uint8_t)j;
   }
   return 0xFF;
 }
@@ -832,7 +914,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
   uint32_t nce, nops, wo = 0, wl = 0, to = 0, tl = 0;
-  const uint32_t bits = msg_level(r, nce, nops, wo, wl, to, tl, s.inl + (size_t)4 * kW2InlEntries * m);
+  const uint32_t bits =
+      msg_level(r, nce, nops, wo, wl, to, tl, s.inl + (size_t)4 * kW2InlEntries * m, s.inl_ops + (size_t)2 * kW2InlOps * m);
   if (bits) nce = nops = 0;
   s.cnt_ce[m] = nce;
   s.cnt_o[m] = nops;
@@ -961,7 +1044,7 @@ __global__ __launch_bounds__(256) void k_w2_mg(
         // the common shape, from the scan: the one grants entry is its key's
         // first and last; its signature is the signature entry if that entry's
         // key is the grant's (walk_mg's lookup over one entry)
-        const bool canon = sc.g.nval <= 1 && grant_canonical(r, sc.g.voff, sc.g.vlen);
+        const bool canon = sc.g.nval <= 1 && sc.g.canon;  // decided by the validating parse
         stp.mark(3);
         if (!canon) {
           bits = kStFb;
@@ -970,7 +1053,7 @@ __global__ __launch_bounds__(256) void k_w2_mg(
           const bool have = sc.nse == 1 && key_eq(r, sc.sg.koff, sc.sg.klen, sc.g.koff, sc.g.klen);
           const uint16_t signer = find_signer(r, sc.sid_off, sc.sid_len, ids, id_off, n_ids, &tab);
           stp.mark(4);
-          const uint8_t slot = find_key_slot(r, s.tx_off[m], s.tx_len[m], sc.g.koff, sc.g.klen);
+          const uint8_t slot = find_key_slot_rec(r, s, m, sc.g.koff, sc.g.klen);
           stp.mark(5);
           rec(sc.g.voff, sc.g.vlen, signer, have && sc.sg.vlen == MOCHI_RSA_BYTES ? sc.sg.voff : ~0u, slot);
         }
@@ -1189,7 +1272,7 @@ inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b
 W2Msg msg_view(const W2Args& a) {
   const size_t m1 = (size_t)a.M + 1;
   uint32_t* p = a.cnt_ce;
-  return W2Msg{p, p + m1, p + 2 * m1, p + 3 * m1, p + 4 * m1, p + 5 * m1, p + 6 * m1, a.cnt_o, a.inl};
+  return W2Msg{p, p + m1, p + 2 * m1, p + 3 * m1, p + 4 * m1, p + 5 * m1, p + 6 * m1, a.cnt_o, a.inl, a.inl_ops};
 }
 
 // grid of the grid-stride certificate-entry kernels (the entry total is on the device)

@@ -1253,12 +1253,14 @@ class ClusterConfig:
     ClusterConfiguration.loadInitialConfigurationFromProperties,
     ClusterConfiguration.java:138-187)."""
 
-    def __init__(self, path: Optional[str] = None, text: Optional[str] = None):
+    def __init__(self, path: Optional[str] = None, text=None):
+        # text: the file's bytes (read as ISO-8859-1, like Properties.load(InputStream)),
+        # or a str, saved as UTF-8 first
         self.lib = load_library()
         if path is not None:
             self.h = self.lib.mochi_config_load(path.encode())
         else:
-            raw = (text or "").encode()
+            raw = text if isinstance(text, (bytes, bytearray)) else (text or "").encode()
             self.h = self.lib.mochi_config_parse(raw, len(raw))
         if not self.h:
             raise MochiError(f"mochi_config: {_err(self.lib)}")

@@ -1,6 +1,8 @@
 """Phase times of k_rsa_pow from a MOCHI_POW_STAMPS build (MOCHI_HIP_LIB points
-at it): per wave, s_memtime cycles per squaring in x^2 (and its middle product M) and in the fold, and the
-kernel's cycles per squaring overall.  One JSON line."""
+at it): per wave, s_memtime cycles per squaring in x^2 and in the fold (each
+between its phase barriers), the grant prep done in the idle half-phases (per
+group), and the kernel's cycles per squaring overall; split by the leading
+(waves 0-3) and lagging (waves 4-7) halves.  One JSON line."""
 import ctypes
 import json
 import os
@@ -31,13 +33,18 @@ lib = ctypes.CDLL(os.environ["MOCHI_HIP_LIB"])
 buf = (ctypes.c_ulonglong * (4096 * 5))()
 assert lib.mochi_debug_pow_stamps(buf, 2048) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 5)[:2048].astype(np.float64)
-a = a[a[:, 3] > 0]
-n = a[:, 3]
-res = {"lib": os.path.basename(os.environ["MOCHI_HIP_LIB"]), "grants": synth.batch.n_grants, "flags_ok": ok,
-       "waves": int(a.shape[0]), "squarings_per_wave": float(n.mean()),
-       "x2_cyc_per_sq": round(float((a[:, 0] / n).mean()), 1), "fold_cyc_per_sq": round(float((a[:, 1] / n).mean()), 1),
-       "x2_middle_cyc_per_sq": round(float((a[:, 4] / n).mean()), 1),
-       "kernel_cyc_per_sq": round(float((a[:, 2] / n).mean()), 1),
-       "x2_p10_p90": [round(float(np.percentile(a[:, 0] / n, q)), 1) for q in (10, 90)],
-       "fold_p10_p90": [round(float(np.percentile(a[:, 1] / n, q)), 1) for q in (10, 90)]}
+wave = np.arange(a.shape[0]) % 8
+keep = a[:, 3] > 0
+res = {"lib": os.path.basename(os.environ["MOCHI_HIP_LIB"]), "grants": synth.batch.n_grants, "flags_ok": ok}
+for name, sel in (("all", keep), ("lead", keep & (wave < 4)), ("lag", keep & (wave >= 4))):
+    b = a[sel]
+    n = b[:, 3]
+    groups = n / 16
+    res[name] = {"waves": int(b.shape[0]), "squarings_per_wave": float(n.mean()),
+                 "x2_cyc_per_sq": round(float((b[:, 0] / n).mean()), 1),
+                 "fold_cyc_per_sq": round(float((b[:, 1] / n).mean()), 1),
+                 "prep_cyc_per_group": round(float((b[:, 4] / groups).mean()), 1),
+                 "kernel_cyc_per_sq": round(float((b[:, 2] / n).mean()), 1),
+                 "x2_p10_p90": [round(float(np.percentile(b[:, 0] / n, q)), 1) for q in (10, 90)],
+                 "fold_p10_p90": [round(float(np.percentile(b[:, 1] / n, q)), 1) for q in (10, 90)]}
 print(json.dumps(res))

@@ -63,6 +63,25 @@ def test_properties_syntax():
     assert cfg.replica_id_list() == ["a", "b", "c", "d"]
 
 
+def test_ids_reach_the_wire_as_java_would_encode_them():
+    """Properties.load(InputStream) reads ISO-8859-1: a raw byte >= 0x80 is one
+    char (2 bytes of UTF-8 on the wire); \\uXXXX escapes are UTF-16 code units, a
+    surrogate pair one supplementary char (4 bytes), a lone surrogate '?'
+    (String.getBytes(UTF_8), protobuf-java's fallback)."""
+    ids = [b"caf\xe9", b"s\\uD83D\\uDE00", b"lone\\uD800x", b"d"]
+    lines = [b"_CONFIG_SERVERS=" + b",".join(ids), b"_CONFIG_BFT_REPLICATION=4"]
+    for s, sid in enumerate(ids):
+        lines.append(b"_CONFIG_SERVER_" + sid + b"_TOKENS=" + ",".join(str(t) for t in range(s, 1024, 4)).encode())
+        lines.append(b"_CONFIG_SERVER_" + sid + b"_URL=127.0.0.1:" + str(8001 + s).encode())
+    cfg = mh.ClusterConfig(text=b"\n".join(lines))
+    want = ["caf\u00e9", "s\U0001F600", "lone?x", "d"]
+    assert [s for s, _ in cfg.servers()] == want
+    assert cfg.replica_id_list() == want
+    blob, off = cfg.replica_ids()
+    assert bytes(blob[off[1]:off[2]]) == "s\U0001F600".encode() and off[2] - off[1] == 5
+    cfg.close()
+
+
 def test_r7_majority():
     ids = [f"s{i}" for i in range(8)]
     cfg = mh.ClusterConfig(text="\n".join(["_CONFIG_SERVERS=" + ",".join(ids), "_CONFIG_BFT_REPLICATION=7"]

@@ -97,16 +97,44 @@ def test_mverify_write2_rejects_grant_level_outputs(pool4):
 
 
 def test_mctx_gathered_bits_are_the_verdicts(pool4):
-    """The all-gather reads each device's accept bitmap where the verify left it:
-    device 0's gathered buffer, assembled, equals the batch's verdict bitmap."""
-    s = W.make_batch(pool4, 4096 + 45, first_cert=5)  # a full 32-aligned shard plus a ragged tail
+    """The all-gather reads each device's accept bitmap where the verify left it.
+    Device 0's gathered buffer, assembled by the shard plan, is checked against
+    verdicts computed WITHOUT it: the oracle's bitmap and a single-context verify
+    of the same batch (not the mctx's own output bits, which gather_bits derives
+    from that same buffer).  Ragged tail: 4,141 certificates."""
+    s = W.make_batch(pool4, 4096 + 45, first_cert=5)
     mv = mh.MultiVerifier(pool4.moduli, _mask())
-    g = mv.verify(s.batch, 4, True)
+    mv.verify(s.batch, 4, True)
     ptr, words = mv.gathered_bits(0)
     n = len(mv.devices)
     plan = mh.shard_plan(s.batch.n_certs, n, s.batch.cert_grant_off)
     got = mh.bits_assemble(plan, _d2h(ptr, n * words))
-    np.testing.assert_array_equal(got[:g.cert_accept_bits.shape[0]], g.cert_accept_bits)
+    o = O.verify_batch(pool4.moduli, s.batch, 4, True, 8)
+    nw = o.cert_accept_bits.shape[0]
+    np.testing.assert_array_equal(got[:nw], o.cert_accept_bits)
+    one = mh.Verifier(pool4.moduli, 0)
+    np.testing.assert_array_equal(got[:nw], one.verify(s.batch, 4, True).cert_accept_bits)
+    one.close()
+    mv.close()
+
+
+def test_mctx_write2_gathered_bits_are_the_verdicts(pool4):
+    """The same for mochi_mverify_write2: the gathered device bitmap after a
+    wire-path verify equals the oracle's decode + verify of the messages."""
+    s = W.make_batch(pool4, 1500 + 13, first_cert=1201)
+    wb = W.encode_wire_batch(s)
+    mv = mh.MultiVerifier(pool4.moduli, _mask())
+    mv.set_server_ids(W.SERVER_IDS[:4])
+    mv.verify_write2(wb, 4, True)
+    ptr, words = mv.gathered_bits(0)
+    n = len(mv.devices)
+    pb = np.concatenate([[0], np.cumsum(wb.msg_len.astype(np.uint64))])  # mochi_mverify_write2's byte prefix
+    plan = mh.shard_plan(wb.n_msgs, n, (pb // (int(pb[-1]) // 0xFFFFFFFF + 1)).astype(np.uint32))
+    got = mh.bits_assemble(plan, _d2h(ptr, n * words))
+    ids, off = W.server_id_table(4)
+    o, _ = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)
+    nw = o.cert_accept_bits.shape[0]
+    np.testing.assert_array_equal(got[:nw], o.cert_accept_bits)
     mv.close()
 
 

@@ -332,6 +332,85 @@ def test_batcher_async_submit(pool4):
     ver.close()
 
 
+def test_batcher_callback_reentry(pool4):
+    """A completion callback may submit to the batcher that runs it (a Java
+    CompletableFuture stage running inline submits the next request): a chain of
+    submissions, each made from the previous one's callback, gets the oracle's
+    verdicts; a blocking verify from a callback is refused with MOCHI_EINVAL; and
+    mochi_batcher_destroy from a callback defers the teardown -- requests already
+    queued still complete, new ones are refused, the last flusher frees it."""
+    import threading
+
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 200, first_cert=9700)
+    wb = W.encode_wire_batch(s)
+    ids, off = W.server_id_table(4)
+    ref, _ = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)
+    M = wb.n_msgs
+    msgs = [wb.wire[int(wb.msg_off[i]):int(wb.msg_off[i]) + int(wb.msg_len[i])].tobytes() for i in range(M)]
+    hashes = [wb.expected_hash[i].tobytes() for i in range(M)]
+    b = mh.Batcher(ver, 4, True, max_msgs=64, max_wait_us=100)
+    res, errs = [None] * M, []
+    fin = threading.Event()
+
+    def chain(i):
+        def done(rc, accepted, reason, fail_op, status):
+            res[i] = (rc, accepted, reason)
+            if i == 0:
+                try:  # blocking from the flusher's own thread: refused, not a deadlock
+                    b.verify(msgs[0], hashes[0])
+                    errs.append("blocking verify from a callback was accepted")
+                except mh.MochiError:
+                    pass
+            try:
+                if i + 1 < M:
+                    b.submit(msgs[i + 1], hashes[i + 1], chain(i + 1))
+                else:
+                    fin.set()
+            except Exception as e:  # noqa: BLE001 -- surfaced by the assert below
+                errs.append(repr(e))
+                fin.set()
+        return done
+
+    b.submit(msgs[0], hashes[0], chain(0))
+    assert fin.wait(120), "callback chain stalled"
+    assert not errs, errs
+    assert all(r is not None and r[0] == mh.OK for r in res)
+    np.testing.assert_array_equal(np.array([r[1] for r in res]), ref.cert_accept)
+    np.testing.assert_array_equal(np.array([r[2] for r in res], np.uint8), ref.cert_reason)
+    b.close()
+
+    # destroy from inside a callback: 32 requests queued, the first callback destroys
+    b2 = mh.Batcher(ver, 4, True, max_msgs=4, max_wait_us=50)
+    got, left, refused = [], [32], []
+    cv = threading.Condition()
+
+    def cb(i):
+        def done(rc, accepted, reason, fail_op, status):
+            if i == 0:
+                b2.lib.mochi_batcher_destroy(b2.h)
+                try:
+                    b2.submit(msgs[40], hashes[40], lambda *a: None)
+                except mh.MochiError:
+                    refused.append(True)
+            with cv:
+                got.append((i, rc, accepted))
+                left[0] -= 1
+                cv.notify()
+        return done
+
+    for i in range(32):
+        b2.submit(msgs[i], hashes[i], cb(i))
+    with cv:
+        assert cv.wait_for(lambda: left[0] == 0, timeout=60), "queued requests lost after a deferred destroy"
+    b2.h = None  # freed by its last flusher
+    assert refused == [True]
+    got.sort()
+    assert [g[1] for g in got] == [mh.OK] * 32
+    np.testing.assert_array_equal(np.array([g[2] for g in got]), ref.cert_accept[:32])
+    ver.close()
+
+
 def _fields(b):
     """(tag, raw field bytes) of a protobuf message with varint / length-delimited fields."""
     out, i = [], 0
