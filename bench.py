@@ -349,7 +349,10 @@ def main():
             "path_cios_equiv_vs_valu_peak": round(value / world * MAC_PER_GRANT / PEAK_MAC_PER_S, 4),
             "stage_ms": {"prep_sha256": round(stage_ms[0], 4), "bucket": round(stage_ms[1], 4),
                          "rsa_pow": round(stage_ms[2], 4), "rsa_final": round(stage_ms[3], 4),
-                         "tally": round(stage_ms[4], 4)},
+                         "tally": round(stage_ms[4], 4),
+                         "note": "prep_sha256 = k_grant_prep + k_grant_deep on the aux stream, launched "
+                                 "beside k_rsa_pow: its blocks run in pow's tail (serialised before it "
+                                 "with MOCHI_PREP_SERIAL=1)"},
             "c3": c3,
             "host_path_pcie_inclusive_grants_per_s": hostp["pinned_grants_per_s"] if hostp else None,
             "host_path": hostp,

@@ -46,17 +46,6 @@ bool prep_serial() {
   return v;
 }
 
-// MOCHI_PREP_KERNEL=1 (A/B and standalone timing): grant prep as its own kernel,
-// beside k_rsa_pow on the aux stream (serialised with MOCHI_PREP_SERIAL=1),
-// instead of inside k_rsa_pow's idle half-phases
-bool prep_kernel() {
-  static const bool v = [] {
-    const char* e = getenv("MOCHI_PREP_KERNEL");
-    return (e && atoi(e) != 0) || prep_serial();
-  }();
-  return v;
-}
-
 uint32_t default_chunk_grants() {
   const char* e = getenv("MOCHI_CHUNK_GRANTS");
   const long x = e ? atol(e) : 0;
@@ -272,7 +261,7 @@ struct mochi_ctx {
   DevBuf dev_in, dev_out;
   PinnedBuf pin_in, pin_out;
   hipStream_t s_in = nullptr, s_out = nullptr;  // host-path copy streams
-  hipStream_t aux = nullptr;                     // grant prep (high priority), overlapped with k_rsa_pow
+  hipStream_t aux = nullptr;                     // grant prep (high priority), beside k_rsa_pow
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // Scratch ordering: every launch that uses the context's scratch waits for
   // the previous one to be done with it (the device entry points are async on a
@@ -349,10 +338,8 @@ int mochi_device_count(void) {
   return n;
 }
 
-// The grant-prep stream runs at the highest priority: its short latency-bound
-// kernel is dispatched ahead of the k_rsa_pow blocks it overlaps, finishes
-// early and hands the CUs back, instead of trickling beside pow for the whole
-// launch (and taking VGPR slots from it).
+// The grant-prep stream runs at the highest priority, so its blocks take each
+// CU the moment k_rsa_pow's block there retires (kernels.hip:launch_verify).
 static hipError_t create_prep_stream(hipStream_t* s) {
   int least = 0, greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
@@ -576,7 +563,6 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.op_ts = o->op_ts;
   a.op_out_off = op_out_off;
   a.aux = prep_serial() ? nullptr : c->aux;  // MOCHI_PREP_SERIAL=1: prep on the launch stream (A/B)
-  a.prep_kernel = prep_kernel();
   a.ev_fork = c->ev_fork;
   a.ev_join = c->ev_join;
   if (c->profiling) {

@@ -55,9 +55,8 @@ struct LaunchArgs {
   // mochi_rsa_public_op only: raw s^65537 mod n words [N][64] (else null)
   uint32_t* dbg_y;
   bool skip_prep_tally;
-  bool prep_kernel;  // grant prep as its own kernel (k_grant_prep) instead of inside k_rsa_pow
   // grant prep runs on `aux` (forked from / joined back to the launch stream
-  // with ev_fork / ev_join) so it overlaps bucketing and k_rsa_pow; null = inline
+  // with ev_fork / ev_join) beside k_rsa_pow; null = serial on the launch stream
   hipStream_t aux;
   hipEvent_t ev_fork, ev_join;
   // optional per-stage timing: a (start, end) event pair per stage, recorded on
@@ -86,8 +85,7 @@ hipError_t launch_rsa_sign(const uint8_t* blob, const uint64_t* goff, const uint
 // Zero every signature whose flags lack MOCHI_GRANT_SIG_OK and count them.
 hipError_t launch_withhold(const uint8_t* flags, uint32_t n, uint8_t* sig, uint32_t* rejected, hipStream_t stream);
 hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t stream);
-struct PrepArgs;
-void launch_rsa_pow(const LaunchArgs& a, const PrepArgs& prep, hipStream_t stream);
+void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream);
 void launch_rsa_final(const LaunchArgs& a, hipStream_t stream);
 void launch_rsa_raw(const LaunchArgs& a, hipStream_t stream);  // dbg_y path (mochi_rsa_public_op)
 

@@ -26,9 +26,96 @@ namespace mochi {
 // ---------------------------------------------------------------------------
 // k_grant_prep: parse + SHA-256, certificate order (lane = grant).
 // ---------------------------------------------------------------------------
+// Lane = grant, and each lane's grant is a different ~150-byte string, so a
+// load straight from HBM touches up to 64 cache lines per instruction (one per
+// lane) and the parse's byte walk is a chain of such loads.  So each wave
+// first stages its 64 grants in LDS -- per grant, the aligned dwords holding
+// it, copied by the whole wave (coalesced: 1-3 lines per load, 8 grants' loads
+// in flight) -- and the lanes then parse and hash from LDS.  A wave whose
+// grants do not fit its share reads them from HBM in place.
+constexpr uint32_t kPrepWaveWords = 3328;  // 13 KB a wave: 3 blocks of 4 waves per CU
+#ifndef MOCHI_PREP_STAGE
+#define MOCHI_PREP_STAGE 1  // 0 (A/B builds): every wave reads HBM in place
+#endif
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 __global__ __launch_bounds__(256) void k_grant_prep(const PrepArgs a) {
+  __shared__ uint32_t stage[4 * kPrepWaveWords];
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t* wst = stage + (threadIdx.x >> 6) * kPrepWaveWords;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.n) grant_prep_one(a, i);
+  const bool have = i < a.n;
+  const uint8_t* p = a.blob + (have ? a.goff[i] : 0);
+  const uint32_t gl = have ? a.glen[i] : 0;
+  const uintptr_t w0 = (uintptr_t)p >> 2;  // the grant's first dword
+  const uint64_t nw64 = gl ? (((uintptr_t)p + gl + 3) >> 2) - w0 : 0;
+  const uint32_t nw = nw64 > kPrepWaveWords ? kPrepWaveWords + 1 : (uint32_t)nw64;
+  uint32_t incl = nw;  // inclusive scan over the wave (at most 64 x 3329: no overflow)
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  const uint32_t off = incl - nw;
+  const bool staged = MOCHI_PREP_STAGE && __shfl(incl, 63) <= kPrepWaveWords;  // wave-uniform
+  if (staged) {
+    const uint32_t wlo = (uint32_t)w0, whi = (uint32_t)((uint64_t)w0 >> 32);
+#pragma unroll 1
+    for (int j0 = 0; j0 < 64; j0 += 8) {
+      uint32_t v[8], sn[8], so[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        sn[u] = __builtin_amdgcn_readlane(nw, j0 + u);
+        so[u] = __builtin_amdgcn_readlane(off, j0 + u);
+        const uint64_t sw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(whi, j0 + u) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane(wlo, j0 + u);
+        v[u] = lane < sn[u] ? GlobalMem::ld32((uintptr_t)(sw << 2) + 4 * lane) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (lane < sn[u]) wst[so[u] + lane] = v[u];
+    }
+#pragma unroll 1
+    for (int j = 0; j < 64; j++) {  // grants longer than 64 dwords: the rest
+      const uint32_t sn = __builtin_amdgcn_readlane(nw, j);
+      if (sn <= 64) continue;
+      const uint32_t so = __builtin_amdgcn_readlane(off, j);
+      const uint64_t sw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(whi, j) << 32) | (uint32_t)__builtin_amdgcn_readlane(wlo, j);
+      for (uint32_t k = 64 + lane; k < sn; k += 64) wst[so + k] = GlobalMem::ld32((uintptr_t)(sw << 2) + 4 * k);
+    }
+  }
+  __syncthreads();  // the staged bytes before any lane reads them (and a fence the compiler keeps)
+  if (!have) return;
+  if (staged) {
+    ByteReaderT<LdsMem> r;
+    r.init_at(p, lds_addr(wst + off), gl);
+    grant_prep_one(a, i, r);
+  } else {
+    ByteReader r;
+    r.init(p, gl);
+    grant_prep_one(a, i, r);
+  }
+}
+
+// the grants k_grant_prep marked kPrepDeep (nested groups deeper than its
+// register stack): CodedInputStream's full 100-deep parse, out of line.  A
+// small grid strides over the flags: the deep parser's stack is scratch
+// memory, which a one-thread-per-grant grid paid for at every wave's launch
+// (1.5 ms for 16M grants, nearly all of them not deep)
+constexpr uint32_t kDeepBlocks = 512;
+__global__ __launch_bounds__(256) void k_grant_deep(const PrepArgs a) {
+#pragma unroll 1
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+    if (a.flags[i] != kPrepDeep) continue;
+    const GrantFields f = parse_grant_deep(a.blob + a.goff[i], a.glen[i]);
+    a.ts[i] = f.ok ? f.ts : 0;
+    a.hash_off[i] = a.goff[i] + f.hash_off;
+    a.hash_len[i] = f.ok ? f.hash_len : 0xFFFFFFFFu;
+    a.flags[i] = f.ok ? MOCHI_GRANT_PARSED : 0;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -456,14 +543,18 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   auto mark = [&](int stage, bool end, hipStream_t s) {
     if (a.prof_events) (void)hipEventRecord(a.prof_events[2 * stage + (end ? 1 : 0)], s);
   };
-  // grant prep (parse + SHA-256) only feeds k_rsa_final and k_tally.  By
-  // default k_rsa_pow does it in the half-phases its SIMD-partner schedule
-  // leaves idle (rsa_pow.hip); with a.prep_kernel it is k_grant_prep, beside
-  // k_rsa_pow on the aux stream (joined before k_rsa_final) or, without aux,
-  // serialised.  That fork comes AFTER bucketing: run beside prep, the short
-  // bucket kernels (which gate k_rsa_pow) took ~4x longer
-  PrepArgs pa{a.blob, a.grant_off, a.grant_len, N, a.digest, a.ts, a.hash_off, a.hash_len, a.flags};
-  const bool prep = N && !a.skip_prep_tally && a.prep_kernel;
+  // Grant prep (parse + SHA-256) only feeds k_rsa_final and k_tally, so it is
+  // forked onto the aux stream after bucketing and joined before k_rsa_final.
+  // k_rsa_pow holds every VGPR of the CUs it runs on (2 waves of 256 per SIMD)
+  // and is dispatched first, so prep's blocks in fact run in pow's TAIL: on
+  // each CU the moment its last pow group is done (the per-CU group counts
+  // differ by one) -- measured 0.8 ms a step better than serialised
+  // (MOCHI_PREP_SERIAL=1).  Done inside k_rsa_pow's phases instead (one wave
+  // per SIMD-half, nothing to hide its latency) it cost the step 5-9 ms
+  // (DESIGN.md section 9).  The fork comes after bucketing: beside prep, the
+  // short bucket kernels (which gate k_rsa_pow) took ~4x longer.
+  const PrepArgs pa{a.blob, a.grant_off, a.grant_len, N, a.digest, a.ts, a.hash_off, a.hash_len, a.flags};
+  const bool prep = N && !a.skip_prep_tally;
   const bool fork = prep && a.aux;
   hipStream_t ps = fork ? a.aux : st;
   mark(kStageBucket, false, st);
@@ -486,16 +577,18 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   mark(kStagePrep, false, ps);
-  if (prep)
+  if (prep) {
     hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
+    const uint32_t db = cdiv(N, 256) < kDeepBlocks ? cdiv(N, 256) : kDeepBlocks;
+    hipLaunchKernelGGL(k_grant_deep, dim3(db), dim3(256), 0, ps, pa);
+  }
   mark(kStagePrep, true, ps);
   if (fork) {
     hipError_t e = hipEventRecord(a.ev_join, a.aux);
     if (e != hipSuccess) return e;
   }
   mark(kStagePow, false, st);
-  if (!(N && !a.skip_prep_tally && !a.prep_kernel)) pa.n = 0;  // prep fused into k_rsa_pow?
-  if (N) launch_rsa_pow(a, pa, st);
+  if (N) launch_rsa_pow(a, st);
   mark(kStagePow, true, st);
   if (fork) {
     hipError_t e = hipStreamWaitEvent(st, a.ev_join, 0);

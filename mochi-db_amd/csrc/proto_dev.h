@@ -7,24 +7,34 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mem_dev.h"
+
 namespace mochi {
 
 // ---------------------------------------------------------------------------
 // Byte access into the grant blob (arbitrary alignment, never reads past the
 // last byte of the grant: the blob may be a slice of a wire buffer).
 // ---------------------------------------------------------------------------
-struct ByteReader {
-  const uint8_t* base;  // grant start
+template <class Mem>
+struct ByteReaderT {
+  using mem = Mem;
+  using addr_t = typename Mem::addr_t;
+  const uint8_t* base;  // grant start in HBM (the deep parser's input)
   uint32_t len;
   uint32_t cached_idx;  // aligned word index (relative to aligned base) held in `w`
   uint32_t w;
-  uintptr_t abase;      // base rounded down to 4
+  addr_t abase;         // the bytes' address rounded down to 4
   uint32_t shift;       // base & 3
 
   __device__ __forceinline__ void init(const uint8_t* p, uint32_t l) {
+    static_assert(sizeof(addr_t) == sizeof(uintptr_t), "HBM reader");
+    init_at(p, (addr_t)(uintptr_t)p & ~(addr_t)3, l);
+  }
+  // the bytes of `p` staged at LDS address `aligned` (p's dword-aligned start)
+  __device__ __forceinline__ void init_at(const uint8_t* p, addr_t aligned, uint32_t l) {
     base = p;
     len = l;
-    abase = (uintptr_t)p & ~(uintptr_t)3;
+    abase = aligned;
     shift = (uint32_t)((uintptr_t)p & 3);
     cached_idx = 0xFFFFFFFFu;
     w = 0;
@@ -34,12 +44,13 @@ struct ByteReader {
     const uint32_t a = i + shift;
     const uint32_t wi = a >> 2;
     if (wi != cached_idx) {
-      w = *(const uint32_t*)(abase + 4 * (uintptr_t)wi);  // word holds byte i: in bounds
+      w = Mem::ld32(abase + 4 * (addr_t)wi);  // word holds byte i: in bounds
       cached_idx = wi;
     }
     return (w >> (8 * (a & 3))) & 0xFFu;
   }
 };
+using ByteReader = ByteReaderT<GlobalMem>;
 
 // ---------------------------------------------------------------------------
 // proto3 Grant parse — restates oracle_grant_parse (oracle/mochi_oracle.c),
@@ -49,7 +60,8 @@ struct ByteReader {
 constexpr int kMaxGroupDepth = 16;    // register-resident group stack of the fast path
 constexpr int kDeepGroupDepth = 100;  // CodedInputStream's default recursion limit (protobuf-java)
 
-__device__ __forceinline__ bool rd_varint(ByteReader& r, uint32_t& pos, uint64_t& v) {
+template <class R>
+__device__ __forceinline__ bool rd_varint(R& r, uint32_t& pos, uint64_t& v) {
   if (pos + 1 < r.len) {  // one- and two-byte varints (tags, lengths) without the loop
     const uint32_t c0 = r.at(pos), c1 = r.at(pos + 1);
     if (c0 < 0x80u) {
@@ -77,7 +89,8 @@ __device__ __forceinline__ bool rd_varint(ByteReader& r, uint32_t& pos, uint64_t
   return false;
 }
 
-__device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
+template <class R>
+__device__ inline bool valid_utf8(R& r, uint32_t off, uint32_t n) {
   uint32_t i = 0;
   // ASCII runs (keys, ids, the 128-char hex transactionHash) 32 bytes per step
   // at any alignment: the 9 aligned words that hold the 32 bytes are loaded
@@ -88,13 +101,14 @@ __device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
   // falls through to the byte-wise UTF-8 check below.
 #pragma unroll 1
   while (i + 32 <= n) {
-    const uintptr_t a = r.abase + (uintptr_t)(off + i + r.shift);
-    const uint32_t* wp = (const uint32_t*)(a & ~(uintptr_t)3);
+    using A = typename R::addr_t;
+    const A a = r.abase + (A)(off + i + r.shift);
+    const A wp = a & ~(A)3;
     const uint32_t sh = (uint32_t)(a & 3);
     uint32_t w[9];
 #pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = wp[k];
-    w[8] = sh ? wp[8] : 0u;
+    for (int k = 0; k < 8; k++) w[k] = R::mem::ld32(wp + 4 * k);
+    w[8] = sh ? R::mem::ld32(wp + 32) : 0u;
     uint32_t hi = w[0] & (0x80808080u << (8 * sh));
 #pragma unroll
     for (int k = 1; k < 8; k++) hi |= w[k];
@@ -106,9 +120,9 @@ __device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
   while (i < n) {
     // 16 ASCII bytes per step once the position is 16-byte aligned (all 16
     // bytes lie inside the string, so the load stays in bounds)
-    const uintptr_t addr = r.abase + (uintptr_t)(off + i + r.shift);
+    const typename R::addr_t addr = r.abase + (typename R::addr_t)(off + i + r.shift);
     if ((addr & 15) == 0 && i + 16 <= n) {
-      const uint4 v = *(const uint4*)addr;
+      const mem_v4u v = R::mem::ld128(addr);
       if (((v.x | v.y | v.z | v.w) & 0x80808080u) == 0) {
         i += 16;
         continue;
@@ -153,7 +167,8 @@ __device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
   return true;
 }
 
-__device__ __forceinline__ bool rd_string(ByteReader& r, uint32_t& pos, uint32_t& off, uint32_t& len) {
+template <class R>
+__device__ __forceinline__ bool rd_string(R& r, uint32_t& pos, uint32_t& off, uint32_t& len) {
   uint64_t l;
   if (!rd_varint(r, pos, l)) return false;
   const int32_t l32 = (int32_t)(uint32_t)l;
@@ -180,8 +195,8 @@ __device__ __forceinline__ uint32_t varint_size(uint64_t v) {
 // none at its default, one-byte tags, minimal varints and lengths, no unknown
 // fields, status an int32 (writeEnum sign-extends) -- decided during the parse
 // instead of a second walk.
-template <int kDepth, bool CANON = false>
-__device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
+template <int kDepth, bool CANON = false, class R>
+__device__ inline bool parse_grant_t(R& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
                                      uint32_t& oid_off, uint32_t& oid_len, bool& too_deep, bool* canon = nullptr) {
   uint32_t pos = 0;
   int64_t t = 0;
@@ -294,7 +309,8 @@ __device__ __noinline__ GrantFields parse_grant_deep(const uint8_t* p, uint32_t 
   return f;
 }
 
-__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
+template <class R>
+__device__ inline bool parse_grant(R& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
                                    uint32_t& oid_len) {
   bool too_deep = false;
   if (parse_grant_t<kMaxGroupDepth>(r, ts, hash_off, hash_len, oid_off, oid_len, too_deep)) return true;
@@ -321,7 +337,8 @@ __device__ inline bool parse_grant_canon(ByteReader& r, bool& canon) {
   return parse_grant_deep(r.base, r.len).ok != 0;
 }
 
-__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
+template <class R>
+__device__ inline bool parse_grant(R& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
   uint32_t oo, ol;
   return parse_grant(r, ts, hash_off, hash_len, oo, ol);
 }

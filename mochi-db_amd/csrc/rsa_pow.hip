@@ -31,13 +31,12 @@
 // (the reverse) much of the time.  So waves 4-7 run one phase behind waves 0-3
 // and a block barrier ends every phase: one wave's x^2 always runs beside its
 // partner's fold, whose MFMAs (at s_setprio 1, so they issue the moment they
-// are ready) co-execute with the x^2's VALU.  Per group each half has one phase
-// with nothing to square (waves 4-7 the first, waves 0-3 the last); those
-// half-phases do the group's GRANT PREP (parse + SHA-256 of 512 grants in
-// certificate order, prep_dev.h) instead of a separate kernel, which the
-// matrix-core kernel, holding every VGPR of the CU, would never let co-reside.
+// are ready) co-execute with the x^2's VALU.  33 phases per group (one
+// half-empty at each end).  Grant prep is its own kernel (kernels.hip): parse
+// and SHA-256 are latency-bound, and in the half-empty phases or the fold's
+// VALU gaps here they ran at one wave per SIMD-half, 2-3x slower than the
+// k_grant_prep launch they replaced.
 #include "fold_dev.h"
-#include "prep_dev.h"
 #include "rsa_common.h"
 
 // MOCHI_POW_STAMPS (measurement builds only, `make ab`): per wave, s_memtime
@@ -46,7 +45,6 @@
 #ifndef MOCHI_POW_STAMPS
 #define MOCHI_POW_STAMPS 0
 #endif
-
 namespace mochi {
 #if MOCHI_POW_STAMPS
 __device__ unsigned long long g_pow_stamps[4096][5];
@@ -54,7 +52,7 @@ __device__ unsigned long long g_pow_stamps[4096][5];
 namespace {
 
 struct Stamps {
-  uint64_t x2 = 0, fold = 0, n = 0, prep = 0;
+  uint64_t x2 = 0, fold = 0, n = 0;
 };
 
 __device__ __forceinline__ uint64_t stamp() {
@@ -85,11 +83,8 @@ struct PowArgs {
 
 // Persistent: one block per CU walks a contiguous range of 512-slot groups, so
 // the CU never idles between blocks and the signer's image is staged only when
-// the key changes along the range (block-uniform).  The block also owns a
-// contiguous range of grants to prep, 512 per group iteration (the ranges are
-// proportional splits of n_slots >= N and of N, so at most one chunk is left
-// for the tail loop).
-__global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a, const PrepArgs pa) {
+// the key changes along the range (block-uniform).
+__global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
   __shared__ v4i w[kFoldImgBytes / 16];
   Stamps st;
   const uint64_t t_begin = stamp();
@@ -102,26 +97,13 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a, const PrepA
   const uint32_t n_groups = (a.n_slots + kBucketAlign - 1) / kBucketAlign;
   const uint32_t g_begin = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
   const uint32_t g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
-  const uint32_t p_begin = (uint32_t)((uint64_t)blockIdx.x * pa.n / gridDim.x);
-  const uint32_t p_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * pa.n / gridDim.x);
-  // this wave's 64 grants of iteration j's chunk
-  auto prep_chunk = [&](uint32_t j) {
-    const uint64_t t0 = stamp();
-    const uint64_t i = (uint64_t)p_begin + (uint64_t)kBucketAlign * j + threadIdx.x;
-    if (i < p_end) grant_prep_one(pa, (uint32_t)i);
-    st.prep += stamp() - t0;
-  };
   uint32_t cur_key = 0xFFFFFFFFu;
   for (uint32_t grp = g_begin; grp < g_end; grp++) {
-    const uint32_t j = grp - g_begin;
     const uint32_t base = grp * kBucketAlign;
     // buckets are 512-aligned and padded only at their tail: a group whose
     // first slot is empty is all padding (every thread reads the same slot)
     const uint32_t g_lead = __builtin_amdgcn_readfirstlane(a.perm[base]);
-    if (g_lead == 0xFFFFFFFFu) {
-      prep_chunk(j);
-      continue;
-    }
+    if (g_lead == 0xFFFFFFFFu) continue;
     const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)a.signer[g_lead]);
     if (key != cur_key) {
       __syncthreads();  // the old image is no longer read
@@ -133,16 +115,12 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a, const PrepA
     const uint32_t slot = base + threadIdx.x;
     const uint32_t g = slot < a.n_slots ? a.perm[slot] : 0xFFFFFFFFu;
     const bool active = g != 0xFFFFFFFFu;
-    if (__ballot(active) == 0) {  // this wave's quarter of the group is padding: prep, keep the barrier count
-      prep_chunk(j);
+    if (__ballot(active) == 0) {  // this wave's quarter of the group is padding: keep the barrier count
 #pragma unroll 1
       for (int i = 0; i < 33; i++) phase_barrier();
       continue;
     }
-    if (lag) {  // phase 0: the partner squares, this wave preps
-      prep_chunk(j);
-      phase_barrier();
-    }
+    if (lag) phase_barrier();  // phase 0: the partner squares, this wave waits its turn
     uint32_t x[kL];
     {
       uint32_t wd[64];
@@ -173,13 +151,8 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a, const PrepA
 #pragma unroll
       for (int q = 0; q < kL; q++) a.zout[(size_t)q * a.n_slots + slot] = x[q];
     }
-    if (!lag) {  // phase 32: the partner folds its last squaring, this wave preps
-      prep_chunk(j);
-      phase_barrier();
-    }
+    if (!lag) phase_barrier();  // phase 32: the partner folds its last squaring
   }
-  // chunks beyond the group range (no squaring left to pair with)
-  for (uint32_t j = g_end - g_begin; (uint64_t)p_begin + (uint64_t)kBucketAlign * j < p_end; j++) prep_chunk(j);
 #if MOCHI_POW_STAMPS
   const uint64_t t_end = stamp();
   const uint32_t wv = blockIdx.x * 8 + (threadIdx.x >> 6);
@@ -188,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a, const PrepA
     g_pow_stamps[wv][1] = st.fold;
     g_pow_stamps[wv][2] = t_end - t_begin;
     g_pow_stamps[wv][3] = st.n;
-    g_pow_stamps[wv][4] = st.prep;
+    g_pow_stamps[wv][4] = 0;
   }
 #else
   (void)t_begin;
@@ -204,10 +177,10 @@ extern "C" int mochi_debug_pow_stamps(unsigned long long* out, unsigned n_waves)
 }
 #endif
 
-void launch_rsa_pow(const LaunchArgs& a, const PrepArgs& prep, hipStream_t st) {
+void launch_rsa_pow(const LaunchArgs& a, hipStream_t st) {
   const uint32_t blocks = fold_grid(a.n_slots);
   const PowArgs pw{a.perm, a.n_slots, a.sig, a.signer, a.fold, a.xbuf};
-  if (blocks) hipLaunchKernelGGL(k_rsa_pow, dim3(blocks), dim3(kBucketAlign), 0, st, pw, prep);
+  if (blocks) hipLaunchKernelGGL(k_rsa_pow, dim3(blocks), dim3(kBucketAlign), 0, st, pw);
 }
 
 }  // namespace mochi
