@@ -350,7 +350,7 @@ def main():
             "stage_ms": {"prep_sha256": round(stage_ms[0], 4), "bucket": round(stage_ms[1], 4),
                          "rsa_pow": round(stage_ms[2], 4), "rsa_final": round(stage_ms[3], 4),
                          "tally": round(stage_ms[4], 4),
-                         "note": "prep_sha256 = k_grant_prep + k_grant_deep on the aux stream, launched "
+                         "note": "prep_sha256 = k_grant_prep on the aux stream, launched "
                                  "beside k_rsa_pow: its blocks run in pow's tail (serialised before it "
                                  "with MOCHI_PREP_SERIAL=1)"},
             "c3": c3,

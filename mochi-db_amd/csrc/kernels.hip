@@ -26,96 +26,9 @@ namespace mochi {
 // ---------------------------------------------------------------------------
 // k_grant_prep: parse + SHA-256, certificate order (lane = grant).
 // ---------------------------------------------------------------------------
-// Lane = grant, and each lane's grant is a different ~150-byte string, so a
-// load straight from HBM touches up to 64 cache lines per instruction (one per
-// lane) and the parse's byte walk is a chain of such loads.  So each wave
-// first stages its 64 grants in LDS -- per grant, the aligned dwords holding
-// it, copied by the whole wave (coalesced: 1-3 lines per load, 8 grants' loads
-// in flight) -- and the lanes then parse and hash from LDS.  A wave whose
-// grants do not fit its share reads them from HBM in place.
-constexpr uint32_t kPrepWaveWords = 3328;  // 13 KB a wave: 3 blocks of 4 waves per CU
-#ifndef MOCHI_PREP_STAGE
-#define MOCHI_PREP_STAGE 1  // 0 (A/B builds): every wave reads HBM in place
-#endif
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
-}
-
 __global__ __launch_bounds__(256) void k_grant_prep(const PrepArgs a) {
-  __shared__ uint32_t stage[4 * kPrepWaveWords];
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t* wst = stage + (threadIdx.x >> 6) * kPrepWaveWords;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool have = i < a.n;
-  const uint8_t* p = a.blob + (have ? a.goff[i] : 0);
-  const uint32_t gl = have ? a.glen[i] : 0;
-  const uintptr_t w0 = (uintptr_t)p >> 2;  // the grant's first dword
-  const uint64_t nw64 = gl ? (((uintptr_t)p + gl + 3) >> 2) - w0 : 0;
-  const uint32_t nw = nw64 > kPrepWaveWords ? kPrepWaveWords + 1 : (uint32_t)nw64;
-  uint32_t incl = nw;  // inclusive scan over the wave (at most 64 x 3329: no overflow)
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d);
-    if (lane >= (uint32_t)d) incl += y;
-  }
-  const uint32_t off = incl - nw;
-  const bool staged = MOCHI_PREP_STAGE && __shfl(incl, 63) <= kPrepWaveWords;  // wave-uniform
-  if (staged) {
-    const uint32_t wlo = (uint32_t)w0, whi = (uint32_t)((uint64_t)w0 >> 32);
-#pragma unroll 1
-    for (int j0 = 0; j0 < 64; j0 += 8) {
-      uint32_t v[8], sn[8], so[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        sn[u] = __builtin_amdgcn_readlane(nw, j0 + u);
-        so[u] = __builtin_amdgcn_readlane(off, j0 + u);
-        const uint64_t sw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(whi, j0 + u) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane(wlo, j0 + u);
-        v[u] = lane < sn[u] ? GlobalMem::ld32((uintptr_t)(sw << 2) + 4 * lane) : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (lane < sn[u]) wst[so[u] + lane] = v[u];
-    }
-#pragma unroll 1
-    for (int j = 0; j < 64; j++) {  // grants longer than 64 dwords: the rest
-      const uint32_t sn = __builtin_amdgcn_readlane(nw, j);
-      if (sn <= 64) continue;
-      const uint32_t so = __builtin_amdgcn_readlane(off, j);
-      const uint64_t sw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(whi, j) << 32) | (uint32_t)__builtin_amdgcn_readlane(wlo, j);
-      for (uint32_t k = 64 + lane; k < sn; k += 64) wst[so + k] = GlobalMem::ld32((uintptr_t)(sw << 2) + 4 * k);
-    }
-  }
-  __syncthreads();  // the staged bytes before any lane reads them (and a fence the compiler keeps)
-  if (!have) return;
-  if (staged) {
-    ByteReaderT<LdsMem> r;
-    r.init_at(p, lds_addr(wst + off), gl);
-    grant_prep_one(a, i, r);
-  } else {
-    ByteReader r;
-    r.init(p, gl);
-    grant_prep_one(a, i, r);
-  }
-}
-
-// the grants k_grant_prep marked kPrepDeep (nested groups deeper than its
-// register stack): CodedInputStream's full 100-deep parse, out of line.  A
-// small grid strides over the flags: the deep parser's stack is scratch
-// memory, which a one-thread-per-grant grid paid for at every wave's launch
-// (1.5 ms for 16M grants, nearly all of them not deep)
-constexpr uint32_t kDeepBlocks = 512;
-__global__ __launch_bounds__(256) void k_grant_deep(const PrepArgs a) {
-#pragma unroll 1
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-    if (a.flags[i] != kPrepDeep) continue;
-    const GrantFields f = parse_grant_deep(a.blob + a.goff[i], a.glen[i]);
-    a.ts[i] = f.ok ? f.ts : 0;
-    a.hash_off[i] = a.goff[i] + f.hash_off;
-    a.hash_len[i] = f.ok ? f.hash_len : 0xFFFFFFFFu;
-    a.flags[i] = f.ok ? MOCHI_GRANT_PARSED : 0;
-  }
+  if (i < a.n) grant_prep_one(a, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -577,11 +490,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   mark(kStagePrep, false, ps);
-  if (prep) {
-    hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
-    const uint32_t db = cdiv(N, 256) < kDeepBlocks ? cdiv(N, 256) : kDeepBlocks;
-    hipLaunchKernelGGL(k_grant_deep, dim3(db), dim3(256), 0, ps, pa);
-  }
+  if (prep) hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
   mark(kStagePrep, true, ps);
   if (fork) {
     hipError_t e = hipEventRecord(a.ev_join, a.aux);

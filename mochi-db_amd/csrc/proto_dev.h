@@ -7,34 +7,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "mem_dev.h"
-
 namespace mochi {
 
 // ---------------------------------------------------------------------------
 // Byte access into the grant blob (arbitrary alignment, never reads past the
 // last byte of the grant: the blob may be a slice of a wire buffer).
 // ---------------------------------------------------------------------------
-template <class Mem>
-struct ByteReaderT {
-  using mem = Mem;
-  using addr_t = typename Mem::addr_t;
-  const uint8_t* base;  // grant start in HBM (the deep parser's input)
+struct ByteReader {
+  const uint8_t* base;  // grant start
   uint32_t len;
   uint32_t cached_idx;  // aligned word index (relative to aligned base) held in `w`
   uint32_t w;
-  addr_t abase;         // the bytes' address rounded down to 4
+  uintptr_t abase;      // base rounded down to 4
   uint32_t shift;       // base & 3
 
   __device__ __forceinline__ void init(const uint8_t* p, uint32_t l) {
-    static_assert(sizeof(addr_t) == sizeof(uintptr_t), "HBM reader");
-    init_at(p, (addr_t)(uintptr_t)p & ~(addr_t)3, l);
-  }
-  // the bytes of `p` staged at LDS address `aligned` (p's dword-aligned start)
-  __device__ __forceinline__ void init_at(const uint8_t* p, addr_t aligned, uint32_t l) {
     base = p;
     len = l;
-    abase = aligned;
+    abase = (uintptr_t)p & ~(uintptr_t)3;
     shift = (uint32_t)((uintptr_t)p & 3);
     cached_idx = 0xFFFFFFFFu;
     w = 0;
@@ -44,13 +34,12 @@ struct ByteReaderT {
     const uint32_t a = i + shift;
     const uint32_t wi = a >> 2;
     if (wi != cached_idx) {
-      w = Mem::ld32(abase + 4 * (addr_t)wi);  // word holds byte i: in bounds
+      w = *(const uint32_t*)(abase + 4 * (uintptr_t)wi);  // word holds byte i: in bounds
       cached_idx = wi;
     }
     return (w >> (8 * (a & 3))) & 0xFFu;
   }
 };
-using ByteReader = ByteReaderT<GlobalMem>;
 
 // ---------------------------------------------------------------------------
 // proto3 Grant parse — restates oracle_grant_parse (oracle/mochi_oracle.c),
@@ -60,21 +49,7 @@ using ByteReader = ByteReaderT<GlobalMem>;
 constexpr int kMaxGroupDepth = 16;    // register-resident group stack of the fast path
 constexpr int kDeepGroupDepth = 100;  // CodedInputStream's default recursion limit (protobuf-java)
 
-template <class R>
-__device__ __forceinline__ bool rd_varint(R& r, uint32_t& pos, uint64_t& v) {
-  if (pos + 1 < r.len) {  // one- and two-byte varints (tags, lengths) without the loop
-    const uint32_t c0 = r.at(pos), c1 = r.at(pos + 1);
-    if (c0 < 0x80u) {
-      v = c0;
-      pos += 1;
-      return true;
-    }
-    if (c1 < 0x80u) {
-      v = (c0 & 0x7Fu) | (c1 << 7);
-      pos += 2;
-      return true;
-    }
-  }
+__device__ __forceinline__ bool rd_varint(ByteReader& r, uint32_t& pos, uint64_t& v) {
   uint64_t x = 0;
 #pragma unroll 1
   for (int i = 0; i < 10; i++) {
@@ -89,8 +64,7 @@ __device__ __forceinline__ bool rd_varint(R& r, uint32_t& pos, uint64_t& v) {
   return false;
 }
 
-template <class R>
-__device__ inline bool valid_utf8(R& r, uint32_t off, uint32_t n) {
+__device__ inline bool valid_utf8(ByteReader& r, uint32_t off, uint32_t n) {
   uint32_t i = 0;
   // ASCII runs (keys, ids, the 128-char hex transactionHash) 32 bytes per step
   // at any alignment: the 9 aligned words that hold the 32 bytes are loaded
@@ -101,14 +75,13 @@ __device__ inline bool valid_utf8(R& r, uint32_t off, uint32_t n) {
   // falls through to the byte-wise UTF-8 check below.
 #pragma unroll 1
   while (i + 32 <= n) {
-    using A = typename R::addr_t;
-    const A a = r.abase + (A)(off + i + r.shift);
-    const A wp = a & ~(A)3;
+    const uintptr_t a = r.abase + (uintptr_t)(off + i + r.shift);
+    const uint32_t* wp = (const uint32_t*)(a & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(a & 3);
     uint32_t w[9];
 #pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = R::mem::ld32(wp + 4 * k);
-    w[8] = sh ? R::mem::ld32(wp + 32) : 0u;
+    for (int k = 0; k < 8; k++) w[k] = wp[k];
+    w[8] = sh ? wp[8] : 0u;
     uint32_t hi = w[0] & (0x80808080u << (8 * sh));
 #pragma unroll
     for (int k = 1; k < 8; k++) hi |= w[k];
@@ -120,9 +93,9 @@ __device__ inline bool valid_utf8(R& r, uint32_t off, uint32_t n) {
   while (i < n) {
     // 16 ASCII bytes per step once the position is 16-byte aligned (all 16
     // bytes lie inside the string, so the load stays in bounds)
-    const typename R::addr_t addr = r.abase + (typename R::addr_t)(off + i + r.shift);
+    const uintptr_t addr = r.abase + (uintptr_t)(off + i + r.shift);
     if ((addr & 15) == 0 && i + 16 <= n) {
-      const mem_v4u v = R::mem::ld128(addr);
+      const uint4 v = *(const uint4*)addr;
       if (((v.x | v.y | v.z | v.w) & 0x80808080u) == 0) {
         i += 16;
         continue;
@@ -167,8 +140,7 @@ __device__ inline bool valid_utf8(R& r, uint32_t off, uint32_t n) {
   return true;
 }
 
-template <class R>
-__device__ __forceinline__ bool rd_string(R& r, uint32_t& pos, uint32_t& off, uint32_t& len) {
+__device__ __forceinline__ bool rd_string(ByteReader& r, uint32_t& pos, uint32_t& off, uint32_t& len) {
   uint64_t l;
   if (!rd_varint(r, pos, l)) return false;
   const int32_t l32 = (int32_t)(uint32_t)l;
@@ -195,8 +167,8 @@ __device__ __forceinline__ uint32_t varint_size(uint64_t v) {
 // none at its default, one-byte tags, minimal varints and lengths, no unknown
 // fields, status an int32 (writeEnum sign-extends) -- decided during the parse
 // instead of a second walk.
-template <int kDepth, bool CANON = false, class R>
-__device__ inline bool parse_grant_t(R& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
+template <int kDepth, bool CANON = false>
+__device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len,
                                      uint32_t& oid_off, uint32_t& oid_len, bool& too_deep, bool* canon = nullptr) {
   uint32_t pos = 0;
   int64_t t = 0;
@@ -309,8 +281,7 @@ __device__ __noinline__ GrantFields parse_grant_deep(const uint8_t* p, uint32_t 
   return f;
 }
 
-template <class R>
-__device__ inline bool parse_grant(R& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
+__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len, uint32_t& oid_off,
                                    uint32_t& oid_len) {
   bool too_deep = false;
   if (parse_grant_t<kMaxGroupDepth>(r, ts, hash_off, hash_len, oid_off, oid_len, too_deep)) return true;
@@ -337,8 +308,7 @@ __device__ inline bool parse_grant_canon(ByteReader& r, bool& canon) {
   return parse_grant_deep(r.base, r.len).ok != 0;
 }
 
-template <class R>
-__device__ inline bool parse_grant(R& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
+__device__ inline bool parse_grant(ByteReader& r, int64_t& ts, uint32_t& hash_off, uint32_t& hash_len) {
   uint32_t oo, ol;
   return parse_grant(r, ts, hash_off, hash_len, oo, ol);
 }

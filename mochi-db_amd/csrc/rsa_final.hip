@@ -140,9 +140,9 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
                                                        uint8_t* __restrict__ flags) {
   __shared__ v4i w[kFoldImgBytes / 16];
   for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
-    // (loading both halves' operands up front -- 483 registers, the second
-    // half's loads in flight during the first half's product -- measured 18 %
-    // slower)
+    // (the next half's operands loaded while this half computes -- into AGPRs,
+    // 445 registers, or both halves up front, 483 -- measured 10 % and 18 %
+    // slower: DESIGN.md section 9)
 #pragma unroll 1
     for (uint32_t h = 0; h < kBucketAlign; h += 256) {
       FinalOps o;

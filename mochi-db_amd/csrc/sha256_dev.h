@@ -4,8 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "mem_dev.h"
-
 namespace mochi {
 
 // ---------------------------------------------------------------------------
@@ -55,31 +53,46 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[
 }
 
 // The 16 message words of block `blk` of the padded message (FIPS 180-4 5.1.1)
-// of the `len` bytes at any alignment.  Words at or past the end take the
-// padding: data bytes, 0x80, zeros, and the 64-bit bit length (len < 2^29) in
-// the last two words of the last block.  The block's bytes come from the 17
-// aligned dwords that hold them, each loaded only if it holds a message byte
-// (so it stays inside the page of a valid byte: the blob may be a slice of a
-// wire buffer), then one funnel shift and a byte swap per word.  `addr0` =
-// the address of message byte 0 in Mem (HBM, or a copy staged in LDS with each
-// byte at its offset mod 4).
-template <class Mem>
-__device__ __forceinline__ void sha256_block_words(typename Mem::addr_t addr0, uint32_t len, uint32_t blk,
-                                                   uint32_t total, uint32_t (&w)[16]) {
-  using A = typename Mem::addr_t;
-  const A addr = addr0 + 64u * blk;
-  const A a4 = addr & ~(A)3;
-  const uint32_t b = (uint32_t)(addr & 3);
-  const int64_t p0 = (int64_t)(64u * blk) - b;  // message position of the first loaded byte
-  uint32_t r[17];
+// of the `len` bytes at `base` (any alignment).  The block's bytes come from
+// 16-byte-aligned dwordx4 loads -- 4 or 5 per block instead of two dword loads
+// and a branch per word -- each issued only if its 16 bytes hold a message
+// byte (so it stays inside the page of a valid byte: the blob may be a slice
+// of a wire buffer), then a per-lane dword rotation (two selects per word,
+// base & 15 is the same for every block), a funnel shift and a byte swap.
+// Words at or past the end take the padding: data bytes, 0x80, zeros, and
+// the 64-bit bit length (len < 2^29) in the last two words of the last block.
+__device__ __forceinline__ void sha256_block_words(const uint8_t* base, uint32_t len, uint32_t blk, uint32_t total,
+                                                   uint32_t (&w)[16]) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const uintptr_t addr = (uintptr_t)base + 64u * blk;
+  const v4u* a16 = (const v4u*)(addr & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(addr & 15);
+  const int64_t p0 = (int64_t)(64u * blk) - sh;  // message position of the first loaded byte
+  uint32_t d[20];
 #pragma unroll
-  for (int i = 0; i < 17; i++)
-    r[i] = (len != 0 && p0 + 4 * i < (int64_t)len && (i < 16 || b != 0)) ? Mem::ld32(a4 + 4 * i) : 0u;
-  const uint32_t sh = 8 * b;
-  const bool full = __ballot(64u * blk + 64 > len) == 0;  // every lane's block is all message bytes
+  for (int c = 0; c < 5; c++) {
+    v4u v = {0u, 0u, 0u, 0u};
+    if (len != 0 && p0 + 16 * c < (int64_t)len && (c < 4 || sh != 0)) v = a16[c];
+    d[4 * c] = v.x;
+    d[4 * c + 1] = v.y;
+    d[4 * c + 2] = v.z;
+    d[4 * c + 3] = v.w;
+  }
+  // e[j] = d[j + (sh >> 2)], j = 0..16, as two rounds of mask selects (a
+  // ternary here is turned into a dynamically indexed array in scratch)
+  const uint32_t m4 = 0u - ((sh >> 2) & 1u), m8 = 0u - ((sh >> 3) & 1u);
+  uint32_t e1[19], e[17];
+#pragma unroll
+  for (int j = 0; j < 19; j++) e1[j] = (d[j + 1] & m4) | (d[j] & ~m4);
+#pragma unroll
+  for (int j = 0; j < 17; j++) e[j] = (e1[j + 2] & m8) | (e1[j] & ~m8);
+  const uint32_t r = 8 * (sh & 3);
+  // every lane's block is all message bytes (the common case): no padding work
+  const bool full = __ballot(64u * blk + 64 > len) == 0;
 #pragma unroll
   for (int t = 0; t < 16; t++) {
-    uint32_t v = __builtin_bswap32(__builtin_amdgcn_alignbit(r[t + 1], r[t], sh));
+    const uint32_t le = __builtin_amdgcn_alignbit(e[t + 1], e[t], r);
+    uint32_t v = __builtin_bswap32(le);
     if (!full) {
       const uint32_t p = 64u * blk + 4u * t;
       if (p + 8 == total) {
@@ -97,8 +110,7 @@ __device__ __forceinline__ void sha256_block_words(typename Mem::addr_t addr0, u
   }
 }
 
-template <class Mem>
-__device__ inline void sha256_at(typename Mem::addr_t addr0, uint32_t len, uint32_t (&h)[8]) {
+__device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8]) {
   h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
   h[4] = 0x510e527f; h[5] = 0x9b05688c; h[6] = 0x1f83d9ab; h[7] = 0x5be0cd19;
   const uint32_t nblocks = (len + 9 + 63) >> 6;
@@ -106,13 +118,9 @@ __device__ inline void sha256_at(typename Mem::addr_t addr0, uint32_t len, uint3
 #pragma unroll 1
   for (uint32_t blk = 0; blk < nblocks; blk++) {
     uint32_t w[16];
-    sha256_block_words<Mem>(addr0, len, blk, total, w);
+    sha256_block_words(base, len, blk, total, w);
     sha256_compress(h, w);
   }
-}
-
-__device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8]) {
-  sha256_at<GlobalMem>((uintptr_t)base, len, h);
 }
 
 }  // namespace mochi

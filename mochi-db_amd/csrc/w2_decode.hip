@@ -51,21 +51,6 @@ struct Fld {
 };
 
 __device__ __forceinline__ bool vint(ByteReader& r, uint32_t& pos, uint32_t end, uint64_t& v) {
-  // one- and two-byte varints (every tag, and every length below 16 KiB) without
-  // the loop: most lanes of a wave take this branch together
-  if (pos + 1 < end) {
-    const uint32_t c0 = r.at(pos), c1 = r.at(pos + 1);
-    if (c0 < 0x80u) {
-      v = c0;
-      pos += 1;
-      return true;
-    }
-    if (c1 < 0x80u) {
-      v = (c0 & 0x7Fu) | (c1 << 7);
-      pos += 2;
-      return true;
-    }
-  }
   uint64_t x = 0;
 #pragma unroll 1
   for (int i = 0; i < 10; i++) {
