@@ -985,9 +985,17 @@ struct W2Stamps {
 #endif
 };
 
-// (capping registers for 4 or 5 waves per SIMD measured 1.4 % and 35 % slower:
-// the walk is instruction-bound, not latency-bound)
-__global__ __launch_bounds__(256) void k_w2_mg(
+#ifndef MOCHI_W2MG_WAVES
+#define MOCHI_W2MG_WAVES 0  // A/B builds: amdgpu_waves_per_eu for k_w2_mg (0 = the compiler's choice)
+#endif
+#if MOCHI_W2MG_WAVES
+#define MOCHI_W2MG_ATTR __attribute__((amdgpu_waves_per_eu(MOCHI_W2MG_WAVES)))
+#else
+#define MOCHI_W2MG_ATTR
+#endif
+// (round 3, at 150 registers: capping for 4 or 5 waves per SIMD measured 1.4 %
+// and 35 % slower)
+__global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
     const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff, const uint32_t* __restrict__ mlen, uint32_t M,
     W2Msg s, CE ce, const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids) {
   __shared__ IdTab tab;
