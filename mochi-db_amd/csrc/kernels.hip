@@ -26,7 +26,15 @@ namespace mochi {
 // ---------------------------------------------------------------------------
 // k_grant_prep: parse + SHA-256, certificate order (lane = grant).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_grant_prep(const PrepArgs a) {
+#ifndef MOCHI_PREP_WAVES
+#define MOCHI_PREP_WAVES 0  // A/B builds: amdgpu_waves_per_eu for k_grant_prep (0 = the compiler's choice)
+#endif
+#if MOCHI_PREP_WAVES
+#define MOCHI_PREP_ATTR __attribute__((amdgpu_waves_per_eu(MOCHI_PREP_WAVES)))
+#else
+#define MOCHI_PREP_ATTR
+#endif
+__global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep(const PrepArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < a.n) grant_prep_one(a, i);
 }
@@ -303,7 +311,16 @@ __device__ bool incoming_cert_ok(const TallyArgs& a, uint32_t c, uint32_t g_lo, 
 // Certificate tally (lane = certificate).  Restates oracle_tally, i.e.
 // InMemoryDataStore.java:613-640 then write2apply :576-611 including the
 // read/apply step (:594-599, :521-574).
-__global__ __launch_bounds__(256) void k_tally(const TallyArgs a) {
+#ifndef MOCHI_TALLY_WAVES
+#define MOCHI_TALLY_WAVES 3  // amdgpu_waves_per_eu (0 = the compiler's choice: 181 VGPRs, 2 waves per SIMD; 3 waves:
+                             // tally 0.63 -> 0.56 ms at C4; 4 waves spill, 0.75 ms)
+#endif
+#if MOCHI_TALLY_WAVES
+#define MOCHI_TALLY_ATTR __attribute__((amdgpu_waves_per_eu(MOCHI_TALLY_WAVES)))
+#else
+#define MOCHI_TALLY_ATTR
+#endif
+__global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs a) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t reason = MOCHI_ACCEPT, fail_op = 0xFF;
   if (c < a.n_certs) {
