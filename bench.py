@@ -88,6 +88,8 @@ def parse_args():
     ap.add_argument("--cache-dir", default=os.environ.get("MOCHI_CACHE", "/tmp/mochi_bench_cache"))
     ap.add_argument("--no-native", action="store_true", help="skip the native batcher load driver leg")
     ap.add_argument("--no-cluster", action="store_true", help="skip the in-process cluster (C1 / C5 proxy) leg")
+    ap.add_argument("--no-shard-sizes", action="store_true", help="skip the per-rank shard-size leg (16M/2, /4, /8)")
+    ap.add_argument("--shard-sizes", action="store_true", help="run the shard-size leg even with --headline-only")
     return ap.parse_args()
 
 
@@ -308,6 +310,9 @@ def main():
         if os.path.exists(batch_file):
             os.remove(batch_file)
         extras = world == 1 and not args.headline_only  # side measurements: single-GPU runs only
+        shard_leg = None
+        if world == 1 and (args.shard_sizes or (extras and not args.no_shard_sizes)):
+            shard_leg = shard_sizes_leg(args, ver, synth, C_total, R, strict, local_rank, stream, stage_ms[2])
         head = W.head_certs(synth, min(C, 1_000_000 // (R * k) * 4)) if extras else None  # ~4M grants
         hostp = host_path(ver, head.batch, R, strict) if extras else None
         wire_s = W.head_certs(synth, min(C, 250_000)) if extras and not args.no_wire else None
@@ -354,6 +359,7 @@ def main():
                                  "beside k_rsa_pow: its blocks run in pow's tail (serialised before it "
                                  "with MOCHI_PREP_SERIAL=1)"},
             "c3": c3,
+            "shard_sizes": shard_leg,
             "host_path_pcie_inclusive_grants_per_s": hostp["pinned_grants_per_s"] if hostp else None,
             "host_path": hostp,
             "write2_wire_path": wire,
@@ -412,6 +418,47 @@ def c3_leg(args, dev, stream):
                      "roofline": roofline(s.batch.n_grants, prof["rsa_pow"])}
     v.close()
     return res
+
+
+def shard_sizes_leg(args, ver, synth, C_total, R, strict, dev, stream, head_pow_ms):
+    """The per-GPU work of the headline at N = 2 / 4 / 8, measured on this GPU:
+    rank 0's shard of the same C4 stream (mochi_shard_plan over the whole
+    batch, contiguous from certificate 0 -- exactly what rank 0 verifies at
+    that N), timed like the headline.  Reports grants/s, per-stage device ms
+    and k_rsa_pow's per-grant cost against the full batch's (strong-scaling
+    ceiling of one rank)."""
+    import numpy as np
+
+    import mochi_hip as mh
+    import workload as W
+
+    N_full = synth.batch.n_grants
+    head_ns = head_pow_ms * 1e6 / N_full
+    rows = []
+    for world in (2, 4, 8):
+        plan = mh.shard_plan(C_total, world)
+        C0 = int(plan[1]) - int(plan[0])
+        s = W.head_certs(synth, C0)
+        d = mh.DeviceBatch(s.batch, dev)
+        o = mh.DeviceVerdicts(d.n_grants, d.n_certs, dev, full=True, n_ops=d.n_ops)
+        ver.set_profiling(True)
+        ev_s, _ = timed_steps(lambda: ver.verify_device(d, o, R, strict, stream=stream.cuda_stream), args.steps,
+                              max(1, args.warmup), stream)
+        ver.set_profiling(False)
+        prof = ver.read_profile()
+        h = o.to_host()
+        n = s.batch.n_grants
+        pow_ns = prof["rsa_pow"] * 1e6 / n
+        rows.append({"world": world, "grants": n, "certs": C0, "grants_per_s": round(n * args.steps / ev_s, 1),
+                     "ms_per_step": round(ev_s / args.steps * 1e3, 4),
+                     "stage_ms": {k: round(prof[k], 4) for k in ver.STAGES},
+                     "pow_ns_per_grant": round(pow_ns, 4), "pow_per_grant_vs_full": round(pow_ns / head_ns, 4),
+                     "roofline_frac": roofline(n, prof["rsa_pow"])["frac"],
+                     "flags_equal_ground_truth": bool(np.array_equal(h.grant_flags, s.expected_flags))})
+        del d, o
+    return {"rows": rows, "full_pow_ns_per_grant": round(head_ns, 4),
+            "note": "rank 0's shard of the C4 stream at each N, on this one GPU (strong scaling: what each rank "
+                    "runs); pow_per_grant_vs_full = k_rsa_pow ns/grant at that size / at 16M"}
 
 
 def host_path(ver, batch, R, strict, reps=3):

@@ -223,6 +223,9 @@ int mochi_device_count(void);
  */
 mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_keys, uint32_t key_bytes,
                             uint32_t public_exponent);
+/* Waits for every batcher built on the context to be freed first (a batcher
+ * destroyed from its own callback is freed by its last flusher thread a little
+ * later), so it must not be called from a callback of such a batcher. */
 void mochi_ctx_destroy(mochi_ctx* ctx);
 
 /*
@@ -576,7 +579,11 @@ int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs);
  * every blocked caller has returned.  From one of the batcher's own callbacks
  * the teardown is deferred instead: later submissions are refused with
  * MOCHI_EINVAL, requests already queued still complete, and the last flusher
- * frees the batcher; the handle must not be used after the call either way. */
+ * frees the batcher; the handle must not be used after the call either way.
+ * The batcher holds its contexts until it is freed: mochi_ctx_destroy on one of
+ * them returns only after that, so a caller that tears down right after its
+ * last callback cannot free a context the flusher still uses.  A process that
+ * exits without destroying the contexts must not exit from a callback. */
 void mochi_batcher_destroy(mochi_batcher* b);
 
 /* ------------------------------------------------------------------------

@@ -31,6 +31,8 @@
 
 namespace mochi {
 int set_error(int code, const std::string& msg);  // capi.cpp: the text mochi_last_error() returns
+void ctx_hold(mochi_ctx* c);                      // capi.cpp: mochi_ctx_destroy waits for the batchers
+void ctx_release(mochi_ctx* c);                   // that hold the context
 }
 
 namespace {
@@ -99,6 +101,16 @@ struct mochi_batcher {
   uint32_t waiters = 0;          // blocking callers not yet out of their wait (mu is theirs until then)
   uint64_t n_batches = 0, n_msgs = 0;
   std::vector<Flusher> fl;
+
+  // Frees the flushers' pinned buffers, then lets the contexts go: however the
+  // batcher ends (joined, or freed by its last flusher after a deferred
+  // destroy), mochi_ctx_destroy on one of its contexts returns only after this.
+  ~mochi_batcher() {
+    std::vector<mochi_ctx*> cs;
+    for (auto& f : fl) cs.push_back(f.ctx);
+    fl.clear();
+    for (mochi_ctx* c : cs) mochi::ctx_release(c);
+  }
 
   // Takes the next batch: waits for work, then for a full batch or for the
   // oldest pending request's deadline (re-evaluated whenever a sibling flusher
@@ -276,7 +288,10 @@ mochi_batcher* mochi_batcher_create_multi(mochi_ctx* const* ctxs, uint32_t n_ctx
   b->max_wait_us = max_wait_us;
   b->fl.resize(n_ctx);
   b->live = n_ctx;
-  for (uint32_t i = 0; i < n_ctx; i++) b->fl[i].ctx = ctxs[i];
+  for (uint32_t i = 0; i < n_ctx; i++) {
+    b->fl[i].ctx = ctxs[i];
+    mochi::ctx_hold(ctxs[i]);
+  }
   for (auto& f : b->fl) {
     Flusher* fp = &f;
     f.th = std::thread([b, fp] { b->run(*fp); });

@@ -13,6 +13,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -249,6 +250,13 @@ int set_error(int code, const std::string& msg) {
 }  // namespace mochi
 
 struct mochi_ctx {
+  // batchers built on this context (mochi_batcher_create*): mochi_ctx_destroy
+  // waits until the last of them is freed -- a batcher destroyed from its own
+  // callback is freed later by its last flusher thread, which still uses the
+  // context's streams and pinned buffers until then
+  std::mutex ref_mu;
+  std::condition_variable ref_cv;
+  int batcher_refs = 0;
   int device = 0;
   hipStream_t stream = nullptr;
   uint32_t n_keys = 0;
@@ -256,7 +264,7 @@ struct mochi_ctx {
   mochi::FoldKey* d_fold = nullptr;  // per-key k_rsa_pow fold matrices (~101 KB each)
   std::mutex mu;
   // verify scratch
-  DevBuf digest, ts, hash_off, hash_len, flags, count, cursor, total, perm, xbuf;
+  DevBuf digest, ts, hash_off, hash_len, flags, count, cursor, total, perm, xbuf, dedup;
   // host-path device copies
   DevBuf dev_in, dev_out;
   PinnedBuf pin_in, pin_out;
@@ -296,6 +304,19 @@ struct mochi_ctx {
 };
 
 namespace mochi {
+// batcher.cpp: a batcher holds each of its contexts from create to its free
+void ctx_hold(mochi_ctx* c) {
+  std::lock_guard<std::mutex> lk(c->ref_mu);
+  c->batcher_refs++;
+}
+void ctx_release(mochi_ctx* c) {
+  {
+    std::lock_guard<std::mutex> lk(c->ref_mu);
+    c->batcher_refs--;
+  }
+  c->ref_cv.notify_all();
+}
+
 // the generation of the last context call made by this thread (multi.cpp reads it
 // right after its mochi_verify_* returns, on the same thread)
 thread_local uint64_t t_ctx_gen = 0;
@@ -411,6 +432,10 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
 
 void mochi_ctx_destroy(mochi_ctx* c) {
   if (!c) return;
+  {  // a batcher on this context still alive (e.g. its deferred teardown not yet done)
+    std::unique_lock<std::mutex> lk(c->ref_mu);
+    c->ref_cv.wait(lk, [&] { return c->batcher_refs == 0; });
+  }
   int save = 0;
   (void)hipGetDevice(&save);
   (void)hipSetDevice(c->device);
@@ -509,11 +534,11 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
   if (slots > 0xFFFFFFF0ull) return fail(MOCHI_EINVAL, "batch too large");
   int rc;
-  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) ||
+  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure(sizeof(uint32_t) * 3 * (size_t)N)) ||
       (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
       (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
       (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
-      (rc = c->total.ensure(sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
+      (rc = c->total.ensure(mochi::kTotalWords * sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
       (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots)))
     return rc;
   mochi::LaunchArgs a;
@@ -554,6 +579,8 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.total = c->total.as<uint32_t>();
   a.perm = c->perm.as<uint32_t>();
   a.xbuf = c->xbuf.as<uint32_t>();
+  a.lead = c->dedup.as<uint32_t>();
+  a.leaders = a.lead + N;
   a.grant_valid_bits = o->grant_valid_bits;
   a.cert_accept_bits = o->cert_accept_bits;
   a.cert_reason = o->cert_reason;
@@ -621,11 +648,11 @@ void par_memcpy(void* dst, const void* src, size_t n) {
 int ensure_scratch(mochi_ctx* c, uint32_t N) {
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
   int rc;
-  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) ||
+  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure(sizeof(uint32_t) * 3 * (size_t)N)) ||
       (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
       (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
       (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
-      (rc = c->total.ensure(sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
+      (rc = c->total.ensure(mochi::kTotalWords * sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
       (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots)))
     return rc;
   return MOCHI_OK;
@@ -1595,7 +1622,7 @@ int mochi_rsa_public_op(mochi_ctx* c, uint32_t n, const uint8_t* sig_be, const u
   if ((rc = c->dev_in.ensure(align_up(sig_bytes, 256) + sizeof(uint16_t) * n)) || (rc = c->dev_out.ensure(y_bytes)) ||
       (rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)n)) || (rc = c->flags.ensure(n)) ||
       (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
-      (rc = c->total.ensure(sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
+      (rc = c->total.ensure(mochi::kTotalWords * sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
       (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots))) {
     (void)hipSetDevice(save);
     return rc;

@@ -40,7 +40,9 @@ struct LaunchArgs {
   uint8_t* flags;      // [N]  (may be the caller's grant_flags output)
   uint32_t* count;     // [n_keys]
   uint32_t* cursor;    // [n_keys]
-  uint32_t* total;     // [1]
+  uint32_t* total;     // [kTotalWords]: bucketed slot total, then per-call counters (zeroed by k_bucket_scan)
+  uint32_t* lead;      // [N] grant dedup: the grant whose prep results g takes (null: no dedup)
+  uint32_t* leaders;   // [2N] (leader, certificate grant end)
   uint32_t* perm;      // [n_slots]
   uint32_t* xbuf;      // [kL][n_slots]
   // outputs
@@ -63,6 +65,9 @@ struct LaunchArgs {
   // the stream the stage runs on
   hipEvent_t* prof_events;
 };
+
+// LaunchArgs::total words
+enum TotalWord { kTotSlots = 0, kTotPowGroup, kTotFinalGroup, kTotNLeaders, kTotPrepChunk, kTotalWords = 8 };
 
 // Stages timed when LaunchArgs::prof_events is set.
 enum ProfStage { kStagePrep = 0, kStageBucket, kStagePow, kStageFinal, kStageTally, kProfStages };

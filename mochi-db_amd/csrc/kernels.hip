@@ -14,6 +14,7 @@
 //   k_pack_bits     grant-valid bitmap via wavefront ballot
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/mochi_hip.h"
 #include "kernels.h"
@@ -37,6 +38,107 @@ namespace mochi {
 __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep(const PrepArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < a.n) grant_prep_one(a, i);
+}
+
+// ---------------------------------------------------------------------------
+// Grant dedup: the R grants of one op key in an honest certificate are the same
+// bytes (every replica builds the Grant from the same objectId, transaction
+// hash and timestamp, InMemoryDataStore.java:131-140), so each distinct grant
+// of a certificate is parsed and hashed once.  k_grant_dedup (lane =
+// certificate) byte-compares every grant with the first grant of its
+// (certificate, op key slot) -- bytes, not offsets: wire-path grants are
+// separate copies -- and lists the distinct ones (leaders) in certificate
+// order; k_grant_prep_lead parses and hashes each leader and stores the same
+// results for the grants that matched it (PrepOut is a function of the bytes).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kDedupMaxGrants = 256;  // larger certificates: every grant its own leader (the slot scan is quadratic)
+
+struct DedupArgs {
+  const uint8_t* blob;
+  const uint64_t* goff;
+  const uint32_t* glen;
+  const uint8_t* grant_key;
+  const uint32_t* cert_grant_off;
+  uint32_t n_certs;
+  uint32_t* lead;     // [N]: the grant whose prep results grant g takes (g itself for a leader)
+  uint32_t* leaders;  // [2 x n_leaders]: (leader, its certificate's grant end)
+  uint32_t* n_leaders;
+};
+
+__global__ __launch_bounds__(256) void k_grant_dedup(const DedupArgs a) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t g_lo = 0, g_hi = 0;
+  if (c < a.n_certs) {
+    g_lo = a.cert_grant_off[c];
+    g_hi = a.cert_grant_off[c + 1];
+  }
+  const bool small = g_hi - g_lo <= kDedupMaxGrants;
+  uint32_t nl = 0;
+#pragma unroll 1
+  for (uint32_t g = g_lo; g < g_hi; g++) {
+    uint32_t L = g;
+    if (small) {
+      const uint32_t s = a.grant_key[g];
+#pragma unroll 1
+      for (uint32_t q = g_lo; q < g; q++)
+        if (a.grant_key[q] == s) {
+          L = q;  // the slot's first grant (a leader by construction)
+          break;
+        }
+      if (L != g) {
+        const uint32_t lg = a.glen[g];
+        const uint64_t og = a.goff[g], ol = a.goff[L];
+        if (lg != a.glen[L] || (og != ol && !bytes_equal(a.blob + og, a.blob + ol, lg))) L = g;
+      }
+    }
+    a.lead[g] = L;
+    nl += L == g;
+  }
+  // leaders of the wave's certificates, in certificate order, at one atomic per wave
+  const uint32_t lane = __lane_id();
+  uint32_t incl = nl;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  const uint32_t tot = __shfl(incl, 63, 64);
+  uint32_t base = 0;
+  if (lane == 0 && tot) base = atomicAdd(a.n_leaders, tot);
+  uint32_t k = __shfl(base, 0, 64) + incl - nl;
+#pragma unroll 1
+  for (uint32_t g = g_lo; g < g_hi && nl; g++)
+    if (a.lead[g] == g) {
+      a.leaders[2 * k] = g;
+      a.leaders[2 * k + 1] = g_hi;
+      k++;
+    }
+}
+
+// Lane = leader, 256-leader chunks taken from a device counter (the blocks run
+// in k_rsa_pow's tail, on CUs that free up at different times).
+__global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_lead(const PrepArgs a, const uint32_t* __restrict__ lead,
+                                                                         const uint32_t* __restrict__ leaders,
+                                                                         const uint32_t* __restrict__ n_leaders,
+                                                                         uint32_t* __restrict__ chunk) {
+  __shared__ uint32_t s_base[2];
+  const uint32_t n = __builtin_amdgcn_readfirstlane(*n_leaders);
+  for (uint32_t it = 0;; it ^= 1) {
+    if (threadIdx.x == 0) s_base[it] = atomicAdd(chunk, blockDim.x);
+    __syncthreads();
+    const uint32_t base = __builtin_amdgcn_readfirstlane(s_base[it]);
+    if (base >= n) break;
+    const uint32_t i = base + threadIdx.x;
+    if (i < n) {
+      const uint32_t L = leaders[2 * i], end = leaders[2 * i + 1];
+      PrepOut o;
+      grant_prep_bytes(a.blob + a.goff[L], a.glen[L], o);
+      grant_prep_store(a, L, o);
+#pragma unroll 1
+      for (uint32_t g = L + 1; g < end; g++)
+        if (lead[g] == L) grant_prep_store(a, g, o);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -102,7 +204,9 @@ __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t* __restrict_
       part[t] = run;
       run += v;
     }
-    *total = run;
+    total[0] = run;
+#pragma unroll
+    for (int i = 1; i < kTotalWords; i++) total[i] = 0;  // the counters of this call's later kernels (kernels.h)
   }
   __syncthreads();
   uint32_t run = part[threadIdx.x];
@@ -458,6 +562,15 @@ __global__ __launch_bounds__(256) void k_withhold(const uint8_t* __restrict__ fl
 // ---------------------------------------------------------------------------
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// MOCHI_NO_DEDUP=1 (A/B): every grant parsed and hashed on its own (k_grant_prep)
+static bool dedup_off() {
+  static const bool off = [] {
+    const char* e = getenv("MOCHI_NO_DEDUP");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
 hipError_t launch_withhold(const uint8_t* flags, uint32_t n, uint8_t* sig, uint32_t* rejected, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_withhold, dim3(cdiv(n, 256)), dim3(256), 0, st, flags, n, sig, rejected);
   return hipGetLastError();
@@ -507,7 +620,18 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   mark(kStagePrep, false, ps);
-  if (prep) hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
+  if (prep) {
+    if (a.lead && a.leaders && a.cert_grant_off && C && !dedup_off()) {
+      const DedupArgs da{a.blob, a.grant_off, a.grant_len, a.grant_key, a.cert_grant_off, C, a.lead, a.leaders,
+                         a.total + kTotNLeaders};
+      hipLaunchKernelGGL(k_grant_dedup, dim3(cdiv(C, 256)), dim3(256), 0, ps, da);
+      const uint32_t pblocks = cdiv(N, 256) < 4096 ? cdiv(N, 256) : 4096;
+      hipLaunchKernelGGL(k_grant_prep_lead, dim3(pblocks), dim3(256), 0, ps, pa, (const uint32_t*)a.lead,
+                         (const uint32_t*)a.leaders, (const uint32_t*)(a.total + kTotNLeaders), a.total + kTotPrepChunk);
+    } else {
+      hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
+    }
+  }
   mark(kStagePrep, true, ps);
   if (fork) {
     hipError_t e = hipEventRecord(a.ev_join, a.aux);

@@ -311,7 +311,11 @@ int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::
   const int n = (int)m->devices.size();
   const uint32_t W = mochi_shard_words((uint32_t)n, cert_lo.data());
   std::vector<int> rc(n, MOCHI_OK);
-  auto work = [&](int i) {
+  // Phase 1 (no collective): every device's gather buffer.  A failure here is
+  // seen by all threads after the join, before any of them enters the
+  // collective, so no device is left waiting in ncclAllGather for a peer that
+  // bailed out.
+  auto prep = [&](int i) {
     if (hipSetDevice(m->devices[i]) != hipSuccess) {
       rc[i] = MOCHI_EHIP;
       return;
@@ -327,6 +331,23 @@ int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::
       }
       m->gathered_cap[i] = bytes;
     }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int i = 0; i < n; i++) th.emplace_back(prep, i);
+    for (auto& t : th) t.join();
+  }
+  for (int r : rc)
+    if (r) return mfail(r, "bitmap all-gather buffers failed");
+  // Phase 2: fill the slot and all-gather.  A local failure filling the slot
+  // (memset, device copy, upload) is recorded, but the device still takes part
+  // in the collective so its peers complete; the error is reported after every
+  // thread has joined.
+  auto work = [&](int i) {
+    if (hipSetDevice(m->devices[i]) != hipSuccess) {
+      rc[i] = MOCHI_EHIP;  // cannot reach the device's stream at all
+      return;
+    }
     uint32_t* slot = m->gathered[i] + (size_t)W * i;
     const uint32_t need = words(cert_lo[i + 1] - cert_lo[i]);  // <= W
     hipError_t e = hipMemsetAsync(slot, 0, 4 * (size_t)W, m->stream[i]);
@@ -341,7 +362,8 @@ int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::
         e = hipMemcpyAsync(slot, shard_bits[i].data(), 4 * have, hipMemcpyHostToDevice, m->stream[i]);
       }
     }
-    if (e != hipSuccess || ncclAllGather(slot, m->gathered[i], W, ncclUint32, m->comm[i], m->stream[i]) != ncclSuccess ||
+    if (e != hipSuccess) rc[i] = MOCHI_EHIP;
+    if (ncclAllGather(slot, m->gathered[i], W, ncclUint32, m->comm[i], m->stream[i]) != ncclSuccess ||
         hipStreamSynchronize(m->stream[i]) != hipSuccess)
       rc[i] = MOCHI_EHIP;
   };

@@ -206,8 +206,12 @@ __device__ inline bool parse_grant_t(ByteReader& r, int64_t& ts, uint32_t& hash_
         const uint32_t p1 = pos;
         if (!rd_varint(r, pos, v)) return false;
         if (tag == 16) t = (int64_t)v;
+        // a 10-byte varint carries bit 63 alone in its last byte: rd_varint
+        // drops bits past 64, so any other last byte (0x02..0x7F) decodes to
+        // the same v but is not what toByteArray() writes
         if (CANON)
-          cn = cn && v != 0 && pos - p1 == varint_size(v) && (tag != 40 || (int64_t)v == (int64_t)(int32_t)(uint32_t)v);
+          cn = cn && v != 0 && pos - p1 == varint_size(v) && (pos - p1 < 10 || r.at(pos - 1) == 1) &&
+               (tag != 40 || (int64_t)v == (int64_t)(int32_t)(uint32_t)v);
         continue;
       }
       if (tag == 34) {

@@ -45,6 +45,11 @@
 #ifndef MOCHI_POW_STAMPS
 #define MOCHI_POW_STAMPS 0
 #endif
+// MOCHI_POW_DYN: blocks take 512-slot groups from a device counter instead of
+// fixed contiguous ranges (A/B)
+#ifndef MOCHI_POW_DYN
+#define MOCHI_POW_DYN 0
+#endif
 namespace mochi {
 #if MOCHI_POW_STAMPS
 __device__ unsigned long long g_pow_stamps[4096][5];
@@ -79,6 +84,7 @@ struct PowArgs {
   const uint16_t* signer;
   const FoldKey* fold;
   uint32_t* zout;
+  uint32_t* ctr;  // MOCHI_POW_DYN group counter
 };
 
 // Persistent: one block per CU walks a contiguous range of 512-slot groups, so
@@ -95,10 +101,21 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
   // wrote (half the signatures wrong)
   const bool lag = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
   const uint32_t n_groups = (a.n_slots + kBucketAlign - 1) / kBucketAlign;
+  uint32_t cur_key = 0xFFFFFFFFu;
+#if MOCHI_POW_DYN
+  // groups from a device counter (zeroed by k_bucket_scan), double-buffered
+  // in LDS so one barrier per fetch suffices
+  __shared__ uint32_t s_grp[2];
+  for (uint32_t it_g = 0;; it_g ^= 1) {
+    if (threadIdx.x == 0) s_grp[it_g] = atomicAdd(a.ctr, 1u);
+    __syncthreads();
+    const uint32_t grp = __builtin_amdgcn_readfirstlane(s_grp[it_g]);
+    if (grp >= n_groups) break;
+#else
   const uint32_t g_begin = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
   const uint32_t g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
-  uint32_t cur_key = 0xFFFFFFFFu;
   for (uint32_t grp = g_begin; grp < g_end; grp++) {
+#endif
     const uint32_t base = grp * kBucketAlign;
     // buckets are 512-aligned and padded only at their tail: a group whose
     // first slot is empty is all padding (every thread reads the same slot)
@@ -179,7 +196,7 @@ extern "C" int mochi_debug_pow_stamps(unsigned long long* out, unsigned n_waves)
 
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t st) {
   const uint32_t blocks = fold_grid(a.n_slots);
-  const PowArgs pw{a.perm, a.n_slots, a.sig, a.signer, a.fold, a.xbuf};
+  const PowArgs pw{a.perm, a.n_slots, a.sig, a.signer, a.fold, a.xbuf, a.total + kTotPowGroup};
   if (blocks) hipLaunchKernelGGL(k_rsa_pow, dim3(blocks), dim3(kBucketAlign), 0, st, pw);
 }
 

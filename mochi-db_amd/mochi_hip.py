@@ -1026,6 +1026,8 @@ class Batcher:
     def submit(self, msg: bytes, expected_hash: bytes, done, op_flags: Optional[bytes] = None):
         """Non-blocking (mochi_batcher_submit): done(rc, accepted, reason, fail_op,
         msg_status) runs on a flusher thread once the message's batch is verified."""
+        if not self.h:
+            raise MochiError("batcher closed")
         key = next(self._seq)
         self._pending[key] = (msg, expected_hash, op_flags, done)  # alive until the callback
         fl = op_flags if op_flags is not None else None
@@ -1074,9 +1076,20 @@ class Batcher:
         return b.value, m.value
 
     def close(self):
-        if self.h:
-            self.lib.mochi_batcher_destroy(self.h)
-            self.h = None
+        """mochi_batcher_destroy, once.  From one of this batcher's callbacks the
+        library defers the teardown (queued requests still complete; its last
+        flusher frees it); the handle is dropped here either way, so a later
+        close() / __del__ cannot free the batcher a second time.  The library
+        holds the contexts until the batcher is freed (mochi_ctx_destroy waits)."""
+        h, self.h = self.h, None
+        if h:
+            self.lib.mochi_batcher_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter teardown
+            pass
 
 
 class DeviceSigner:
@@ -1248,6 +1261,22 @@ class Comm:
             self.h = None
 
 
+def properties_bytes(text: str) -> bytes:
+    """A str as the bytes of a properties file Properties.load(InputStream) reads
+    back as that str: ISO-8859-1 for U+0000..U+00FF, a \\uXXXX escape per UTF-16
+    code unit above (a supplementary character becomes its surrogate pair)."""
+    out = bytearray()
+    for ch in text:
+        cp = ord(ch)
+        if cp <= 0xFF:
+            out.append(cp)
+        else:
+            u = ch.encode("utf-16-be", "surrogatepass")
+            for i in range(0, len(u), 2):
+                out += b"\\u%04X" % int.from_bytes(u[i:i + 2], "big")
+    return bytes(out)
+
+
 class ClusterConfig:
     """The reference's cluster properties file (mochi_config_*;
     ClusterConfiguration.loadInitialConfigurationFromProperties,
@@ -1255,12 +1284,14 @@ class ClusterConfig:
 
     def __init__(self, path: Optional[str] = None, text=None):
         # text: the file's bytes (read as ISO-8859-1, like Properties.load(InputStream)),
-        # or a str, saved as UTF-8 first
+        # or a str, written the way Properties.store would: ISO-8859-1, every
+        # character above U+00FF as a \\uXXXX escape (UTF-16 units), so an id given
+        # as a str reads back as that same str (not its UTF-8 bytes re-read as Latin-1)
         self.lib = load_library()
         if path is not None:
             self.h = self.lib.mochi_config_load(path.encode())
         else:
-            raw = text if isinstance(text, (bytes, bytearray)) else (text or "").encode()
+            raw = text if isinstance(text, (bytes, bytearray)) else properties_bytes(text or "")
             self.h = self.lib.mochi_config_parse(raw, len(raw))
         if not self.h:
             raise MochiError(f"mochi_config: {_err(self.lib)}")

@@ -10,6 +10,8 @@
 #   bench        the default bench (C4 headline + every leg) -> gpurun_out/bench.json
 #   ab           headline-only bench, in-tree lib vs each of $AB_LIBS, alternated twice
 #                (AB_ENV="A=... B=..." per-variant env overrides are not supported: use libs)
+#   abenv        headline-only bench, default env vs each ';'-separated env setting of
+#                $AB_ENVS (e.g. AB_ENVS="MOCHI_NO_DEDUP=1;MOCHI_PREP_SERIAL=1"), alternated twice
 #   kt           rocprofv3 kernel trace + stats of the headline (-> gpurun_out/prof_kt)
 #   pmc          the PMC passes (scripts/pmc.sh)
 #   w2           wire-path tests + kernel trace of the device decoder (w2_prof.py)
@@ -49,6 +51,15 @@ for step in "$@"; do
         if [ $v = A ]; then L=""; t=A; else L="$PWD/$v"; t=$(basename $v .so); fi
         MOCHI_HIP_LIB=$L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --headline-only ${BENCH_ARGS:-} > $OUT/ab_$t$i.json 2> $OUT/ab_$t$i.err || fail ab $OUT/ab_$t$i.err
         python -c "import json;d=json.load(open('$OUT/ab_$t$i.json'));print('$t$i', round(d['value']/1e6,2),'M grants/s', d['ms_per_step'], d['stage_ms'], 'ok=',d.get('correct_vs_ground_truth'))"
+      done
+    done ;;
+  abenv)
+    IFS=';' read -ra ENVS <<< "${AB_ENVS}"
+    for i in 1 2; do
+      for j in $(seq 0 ${#ENVS[@]}); do
+        if [ $j = 0 ]; then E=""; t=A; else E="${ENVS[$((j-1))]}"; t="E$j"; fi
+        env $E timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --headline-only ${BENCH_ARGS:-} > $OUT/abenv_$t$i.json 2> $OUT/abenv_$t$i.err || fail abenv $OUT/abenv_$t$i.err
+        python -c "import json;d=json.load(open('$OUT/abenv_$t$i.json'));print('$t$i [$E]', round(d['value']/1e6,2),'M grants/s', d['ms_per_step'], d['stage_ms'], 'ok=',d.get('correct_vs_ground_truth'))"
       done
     done ;;
   kt)

@@ -373,12 +373,39 @@ class Pending:
     replies: Dict[int, object] = field(default_factory=dict)
     dead: set = field(default_factory=set)  # servers that threw (no reply)
     t_start: float = 0.0
+    outstanding: int = 0  # async Write2s delivered but not yet applied (async_w2 mode)
+
+
+@dataclass
+class AsyncW2:
+    """A Write2 in the asynchronous handler: the state
+    snapshot it was submitted with, and its verdict once the callback ran."""
+    srv: "Server"
+    p: Pending
+    snap: Tuple[list, list]
+    verdict: Optional[tuple] = None
+    req: object = None
+    submits: int = 0
 
 
 class Cluster:
     def __init__(self, backend: str = "device", check_oracle: bool = False, seed: int = 1, device: int = 0,
-                 config_path: str = SAMPLE_CONFIG, key_dir: str = W.DEFAULT_KEY_DIR, max_wait_us: int = 200):
+                 config_path: str = SAMPLE_CONFIG, key_dir: str = W.DEFAULT_KEY_DIR, max_wait_us: int = 200,
+                 async_w2: bool = False, p_apply: float = 0.35):
+        """async_w2: Write2s go through INTEGRATION.md §4's asynchronous handler -- the
+        server snapshots the verifier's inputs (op flags, stored-certificate
+        timestamps) under the key locks, RELEASES them and submits; the verdict
+        is applied at a later step (each ready completion with probability
+        p_apply), after re-checking the state under the locks
+        (sameWrite2State) and re-submitting when a Write2 on one of the keys
+        landed meanwhile.  Several Write2s on one key at one server are then in
+        flight together.  Every state change is logged (self.log) for
+        replay_serial()."""
         assert backend in ("device", "host")
+        self.async_w2 = async_w2
+        self.p_apply = p_apply
+        self.async_q: List[AsyncW2] = []
+        self.log: List[tuple] = []
         self.backend = backend
         self.check_oracle = check_oracle
         self.rng = random.Random(seed)
@@ -411,7 +438,8 @@ class Cluster:
         self.inflight: List[Pending] = []
         self.n_clients = 0
         self.stats = {"write1": 0, "write2": 0, "reads": 0, "retries": 0, "oracle_checked": 0, "steps": 0,
-                      "signed": 0, "read_branch": 0}
+                      "signed": 0, "read_branch": 0, "resubmits": 0, "max_same_key_inflight": 0}
+        self.config_path = config_path
 
     def close(self):
         if self.batcher:
@@ -518,6 +546,65 @@ class Cluster:
             assert g == w, f"library {g} != oracle {w} (server {s.index}, flags {f}, ts {t})"
         self.stats["oracle_checked"] += len(jobs)
 
+    # --- the asynchronous Write2 handler ------------------------
+    def _async_submit(self, es: List[AsyncW2]):
+        """Submit each entry with its snapshot; returns once every verdict is in
+        (the callbacks ran), so the scheduler's choices stay deterministic."""
+        if not es:
+            return
+        for e in es:
+            e.submits += 1
+            e.verdict = None
+        if self.backend == "device":
+            done = threading.Semaphore(0)
+            for e in es:
+                flags, ots = e.snap
+                e.req = mh.Write2Request(e.p.msg, e.p.thash.encode(), flags, ots)
+                self.batcher.submit_request(e.req, lambda _r: done.release())  # callback on a flusher thread
+            for _ in es:
+                done.acquire()
+            for e in es:
+                rc, acc, reason, fail_op, _ = e.req.result
+                assert rc == mh.OK, rc
+                e.verdict = (acc, reason, fail_op, e.req.ops())
+            if self.check_oracle:
+                self._oracle_check([(e.srv, e.p, e.snap[0], e.snap[1]) for e in es], [e.verdict for e in es])
+        else:
+            for e, v in zip(es, self._oracle_verdicts([(e.srv, e.p, e.snap[0], e.snap[1]) for e in es])):
+                e.verdict = v
+
+    def _async_complete(self):
+        """The apply tasks of ready verdicts, a random subset per step, each under
+        its keys' locks (atomic here): unchanged state -> apply the verdict and
+        reply; changed -> verify again against the new state."""
+        again = []
+        ready = [e for e in self.async_q if e.verdict is not None]
+        self.rng.shuffle(ready)
+        for e in ready:
+            if self.rng.random() >= self.p_apply:
+                continue
+            cur = e.srv.write2_state(e.p.ops)
+            if cur != e.snap:  # sameWrite2State failed: a Write2 on one of the keys landed meanwhile
+                e.snap = cur
+                self.stats["resubmits"] += 1
+                again.append(e)
+                continue
+            self.async_q.remove(e)
+            self._apply_w2(e.srv, e.p, e.verdict)
+            e.p.outstanding -= 1
+        self._async_submit(again)
+
+    def _apply_w2(self, srv, p, verdict):
+        acc, reason, fail_op, per_op = verdict
+        self.stats["write2"] += 1
+        self.stats["read_branch"] += sum(1 for d, _, _ in per_op if d == mh.OPD_READ)
+        res = srv.write2_apply(p.ops, p.cert, acc, per_op)
+        self.log.append((srv.index, "W2", p, res))
+        if res is None:
+            p.dead.add(srv.index)
+        else:
+            p.replies[srv.index] = res
+
     # --- client API ------------------------------------------------------------------
     def new_client(self) -> int:
         self.n_clients += 1
@@ -555,15 +642,24 @@ class Cluster:
                 if self.rng.random() < p_deliver:
                     deliveries.append((p, s))
         if not deliveries:  # always make progress
-            p = self.inflight[0]
-            deliveries.append((p, p.todo[0]))
+            p = next((q for q in self.inflight if q.todo), None)
+            if p is not None:
+                deliveries.append((p, p.todo[0]))
         self.rng.shuffle(deliveries)
         # one Write2 per (server, key) per step (the object's write lock serialises them)
         locked = set()
         w1_new: Dict[int, List[GrantRec]] = {}
         w2_jobs = []
+        submit_now = []
         for p, s in deliveries:
             srv = self.servers[s]
+            if p.kind == "W2" and self.async_w2:  # snapshot under the locks, release, submit
+                e = AsyncW2(srv, p, srv.write2_state(p.ops))
+                self.async_q.append(e)
+                submit_now.append(e)
+                p.outstanding += 1
+                p.todo.remove(s)
+                continue
             if p.kind == "W2":
                 keys = {(s, op.key) for op in p.ops}
                 if keys & locked:
@@ -577,10 +673,13 @@ class Cluster:
                 kind, mg, new = srv.write1(p.ops, p.seed, p.thash, "")
                 w1_new.setdefault(s, []).extend(new)
                 p.replies[s] = (kind, mg)
+                self.log.append((s, "W1", p, (kind, [(g.object_id, g.ts, g.txn_hash, g.status) for g in mg.grants],
+                                            p.seed)))
             else:
                 if any((s, op.key) in locked for op in p.ops):
                     continue
                 res = srv.read(p.ops)
+                self.log.append((s, "R", p, res))
                 if res is None:
                     p.dead.add(s)
                 else:
@@ -588,21 +687,24 @@ class Cluster:
             p.todo.remove(s)
         for s, grants in w1_new.items():  # the Write1 site signs every grant it issues
             self._sign(self.servers[s], grants)
-        for (srv, p, flags, ots), (acc, reason, fail_op, per_op) in zip(w2_jobs, self._verify_write2(w2_jobs)):
-            self.stats["write2"] += 1
-            self.stats["read_branch"] += sum(1 for d, _, _ in per_op if d == mh.OPD_READ)
-            res = srv.write2_apply(p.ops, p.cert, acc, per_op)
-            if res is None:
-                p.dead.add(srv.index)
-            else:
-                p.replies[srv.index] = res
+        for (srv, p, flags, ots), v in zip(w2_jobs, self._verify_write2(w2_jobs)):
+            self._apply_w2(srv, p, v)
+        if self.async_w2:
+            self._async_submit(submit_now)
+            per_key: Dict[tuple, int] = {}
+            for e in self.async_q:
+                for k in {op.key for op in e.p.ops}:
+                    per_key[(e.srv.index, k)] = per_key.get((e.srv.index, k), 0) + 1
+            if per_key:
+                self.stats["max_same_key_inflight"] = max(self.stats["max_same_key_inflight"], max(per_key.values()))
+            self._async_complete()
         return self._advance()
 
     def _advance(self):
         finished = []
         w1_rounds, tallies = [], []
         for p in list(self.inflight):
-            if p.todo:
+            if p.todo or p.outstanding:
                 continue
             self.inflight.remove(p)
             if p.dead:
@@ -664,6 +766,39 @@ class Cluster:
 
     def execute_read(self, client: int, ops: List[Op]) -> List[OpResult]:
         return self.run(self.start_read(client, ops))
+
+
+def _state(servers):
+    return {(s.index, k): (sv.value, sv.available, id(sv.current_c) if sv.current_c is not None else None, sv.epoch,
+                           tuple(sorted(sv.given)))
+            for s in servers for k, sv in s.store.items()}
+
+
+def replay_serial(c: Cluster) -> int:
+    """Replay cluster c's logged server events (Write1 deliveries, Write2 applies,
+    reads), in the order they changed state, on fresh servers with every Write2
+    verified serially by the CPU oracle against the replayed state -- the
+    reference's order of events, each Write2 validated and applied under its
+    keys' write locks (InMemoryDataStore.java:641-666, StoreValueObjectContainer.java:229-251).
+    Asserts every reply and the final per-key state (value, availability,
+    currentC, epoch, given grants) equal c's.  Returns the events checked."""
+    cfg = mh.ClusterConfig(c.config_path)
+    servers = [Server(i, sid, url, c.replica_ids) for i, (sid, url) in enumerate(cfg.servers())]
+    cfg.close()
+    for n, (si, kind, p, got) in enumerate(c.log):
+        srv = servers[si]
+        if kind == "W1":
+            k, mg, _ = srv.write1(p.ops, got[2], p.thash, "")
+            want = (k, [(g.object_id, g.ts, g.txn_hash, g.status) for g in mg.grants], got[2])
+        elif kind == "R":
+            want = srv.read(p.ops)
+        else:
+            flags, ots = srv.write2_state(p.ops)
+            acc, _, _, per_op = c._oracle_verdicts([(srv, p, flags, ots)])[0]
+            want = srv.write2_apply(p.ops, p.cert, acc, per_op)
+        assert want == got, f"event {n} ({kind} at server {si}): serial replay {want} != {got}"
+    assert _state(servers) == _state(c.servers), "final per-key state differs from the serial replay"
+    return len(c.log)
 
 
 def write_ops(*kv) -> List[Op]:

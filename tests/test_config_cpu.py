@@ -82,6 +82,21 @@ def test_ids_reach_the_wire_as_java_would_encode_them():
     cfg.close()
 
 
+def test_str_text_round_trips_ids():
+    """ClusterConfig(text=str) writes the str the way Properties.store
+    would (ISO-8859-1, \\uXXXX above U+00FF), so the ids read back as the same str
+    -- not as its UTF-8 bytes re-read as Latin-1 ('caf\u00c3\u00a9')."""
+    ids = ["caf\u00e9", "s\U0001F600", "\u4e2d", "d"]
+    lines = ["_CONFIG_SERVERS=" + ",".join(ids), "_CONFIG_BFT_REPLICATION=4"]
+    for s, sid in enumerate(ids):
+        lines.append(f"_CONFIG_SERVER_{sid}_TOKENS=" + ",".join(str(t) for t in range(s, 1024, 4)))
+        lines.append(f"_CONFIG_SERVER_{sid}_URL=127.0.0.1:{8001 + s}")
+    cfg = mh.ClusterConfig(text="\n".join(lines))
+    assert [s for s, _ in cfg.servers()] == ids
+    assert cfg.replica_id_list() == ids
+    cfg.close()
+
+
 def test_r7_majority():
     ids = [f"s{i}" for i in range(8)]
     cfg = mh.ClusterConfig(text="\n".join(["_CONFIG_SERVERS=" + ",".join(ids), "_CONFIG_BFT_REPLICATION=7"]

@@ -436,3 +436,89 @@ def test_grant_group_depth_matches_google_protobuf(pool4, ver4, golden_dir):
         assert g.grant_flags[i] & mh.GRANT_SIG_OK  # signature fine either way
         if v["expect"]["ok"]:
             assert g.grant_ts[i] == v["expect"]["timestamp"], v["name"]
+
+
+def _dedup_batch(pems, certs, shared_first=False):
+    """certs: list of lists of (grant bytes, signer, key slot); every grant its own copy
+    in the blob at a varying alignment (the byte-compare path of k_grant_dedup), or --
+    with shared_first -- grants equal to the certificate's first one pointing at its
+    bytes (the SoA layout's offset shortcut)."""
+    blob = bytearray(b"\x07")
+    offs, lens, sigs, signer, gkey, cgo = [], [], [], [], [], [0]
+    cop, opk = [0], []
+    for ci, cert in enumerate(certs):
+        first = None
+        for gi, (gb, s, k) in enumerate(cert):
+            if shared_first and first is not None and gb == first[0]:
+                offs.append(first[1])
+            else:
+                blob += b"\xee" * ((ci + gi) % 4)
+                offs.append(len(blob))
+                blob += gb
+                if first is None:
+                    first = (gb, offs[-1])
+            lens.append(len(gb))
+            sigs.append(O.rsa_sign(pems[s], gb))
+            signer.append(s)
+            gkey.append(k)
+        cgo.append(len(offs))
+        keys = sorted({k for _, _, k in cert})
+        opk += keys
+        cop.append(len(opk))
+    n, C = len(offs), len(certs)
+    th = W.txn_hash_hex(9)
+    return mh.Batch(grant_bytes=np.frombuffer(bytes(blob), np.uint8).copy(), grant_off=np.array(offs, np.uint64),
+                    grant_len=np.array(lens, np.uint32), sig=np.frombuffer(b"".join(sigs), np.uint8).reshape(n, 256).copy(),
+                    signer=np.array(signer, np.uint16), grant_key=np.array(gkey, np.uint8),
+                    cert_grant_off=np.array(cgo, np.uint32), cert_op_off=np.array(cop, np.uint32),
+                    op_key=np.array(opk, np.uint8), op_flags=np.full(len(opk), 3, np.uint8),
+                    expected_hash=np.stack([np.frombuffer(th.encode(), np.uint8)] * C))
+
+
+@pytest.mark.parametrize("shared_first", [False, True])
+def test_grant_dedup_one_byte_differences(pool4, ver4, shared_first):
+    """Grant prep hashes each distinct grant of a (certificate, key slot) once
+    (k_grant_dedup + k_grant_prep_lead).  Grants that differ from the slot's first
+    grant in exactly one byte -- timestamp skew, a g1 / g0 transactionHash mismatch, a
+    flipped objectId byte, a trailing unknown field -- must be prepped on their own:
+    flags, timestamps and verdicts bit-exact with the oracle (which hashes every
+    grant)."""
+    pems = W.load_keys(4)
+    th = W.txn_hash_hex(9)
+    oth = th[:-1] + ("0" if th[-1] != "0" else "1")
+    base = W.encode_grant("DEMO_KEY_DEDUP", 1000, th)
+    skew = W.encode_grant("DEMO_KEY_DEDUP", 1001, th)
+    hmis = W.encode_grant("DEMO_KEY_DEDUP", 1000, oth)
+    oflip = W.encode_grant("DEMO_KEY_DEDUQ", 1000, th)
+    longer = base + b"\x30\x01"  # unknown varint field 6: parses, not byte-equal
+    assert all(len(x) == len(base) for x in (skew, hmis, oflip))
+    variants = {"honest": [base] * 4, "ts_skew": [base, base, skew, base], "g1_hash": [base, hmis, base, base],
+                "g0_hash": [hmis, base, base, base], "oid_flip": [base, base, base, oflip],
+                "longer": [base, longer, base, base], "all_skew": [base, skew, skew, skew]}
+    certs = []
+    for _ in range(40):  # enough certificates for several waves of k_grant_dedup lanes
+        for gs in variants.values():
+            certs.append([(gb, r, 0) for r, gb in enumerate(gs)])
+    # two key slots in one certificate (k = 2), interleaved
+    certs.append([(base, 0, 0), (skew, 0, 1), (base, 1, 0), (skew, 1, 1), (base, 2, 0), (skew, 2, 1)])
+    b = _dedup_batch(pems, certs, shared_first)
+    for strict in (True, False):
+        g = ver4.verify(b, 4, strict)
+        o = O.verify_batch(pool4.moduli, b, 4, strict, 2)
+        assert_same(g, o, f"strict={strict}")
+    assert (g.grant_flags & 1).all()  # every signature is valid
+    reasons = {k: int(g.cert_reason[i]) for i, k in enumerate(variants)}
+    assert reasons["honest"] == mh.ACCEPT and reasons["ts_skew"] == mh.REJECT_TS_MISMATCH
+    assert reasons["g0_hash"] == mh.REJECT_HASH_MISMATCH
+
+
+def test_grant_dedup_large_certificate(pool4, ver4):
+    """A certificate above k_grant_dedup's slot-scan bound (256 grants) is prepped grant
+    by grant; results equal the oracle's."""
+    pems = W.load_keys(4)
+    th = W.txn_hash_hex(9)
+    gs = [W.encode_grant("DEMO_KEY_BIG", 1000 + (i % 3 == 2), th) for i in range(300)]
+    b = _dedup_batch(pems, [[(gb, i % 4, 0) for i, gb in enumerate(gs)], [(gs[0], r, 0) for r in range(4)]])
+    g = ver4.verify(b, 4, True)
+    o = O.verify_batch(pool4.moduli, b, 4, True, 2)
+    assert_same(g, o)

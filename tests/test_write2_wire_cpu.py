@@ -189,3 +189,22 @@ def test_oracle_fast_path_counts_wire_entries():
         assert int(f["msg_status"][0]) == 0, name
         assert int(f["cert_mg_off"][1]) == n_mgs_full, name
         assert int(f["cert_grant_off"][1]) == n_mgs_full, name  # one distinct grant per MultiGrant
+
+
+def test_oracle_ten_byte_varint_garbage_not_canonical():
+    """A negative timestamp's 10-byte varint ends in 0x01; with 0x03 instead the
+    Grant parses to the same fields but is not Grant.toByteArray(), so the decoder's
+    fast path declines it (FALLBACK, 2) while the canonical form decodes (OK, 0).
+    The device twin is tests/test_write2_wire_gpu.py."""
+    ids, off = W.server_id_table(4)
+    oid = "DEMO_KEY_NEG_TS"
+    canon = W.encode_grant(oid, -5, "ab" * 64)
+    v = W._varint(-5)
+    bad = canon.replace(b"\x10" + v, b"\x10" + v[:-1] + b"\x03")
+    st = []
+    for gb in (canon, bad):
+        ent = [(W.SERVER_IDS[r], W.encode_multigrant([(oid, gb)], W.SERVER_IDS[r], "cl", "", [(oid, b"\x00" * 256)]))
+               for r in range(4)]
+        d = O.w2_decode(_single(W.encode_write2(ent, [W.encode_operation(2, oid)])), ids, off)
+        st.append(int(d["msg_status"][0]))
+    assert st == [0, 2], st

@@ -388,7 +388,13 @@ def test_batcher_callback_reentry(pool4):
     def cb(i):
         def done(rc, accepted, reason, fail_op, status):
             if i == 0:
-                b2.lib.mochi_batcher_destroy(b2.h)
+                h = b2.h
+                b2.close()  # deferred: this callback runs on one of b2's flushers
+                # the library refuses a submission after the (deferred) destroy; the
+                # batcher is alive at least until this callback returns
+                rc = b2.lib.mochi_batcher_submit(h, msgs[40], len(msgs[40]), None, 0, hashes[40], b2._cb, 0)
+                if rc == mh.EINVAL:
+                    refused.append(True)
                 try:
                     b2.submit(msgs[40], hashes[40], lambda *a: None)
                 except mh.MochiError:
@@ -403,8 +409,9 @@ def test_batcher_callback_reentry(pool4):
         b2.submit(msgs[i], hashes[i], cb(i))
     with cv:
         assert cv.wait_for(lambda: left[0] == 0, timeout=60), "queued requests lost after a deferred destroy"
-    b2.h = None  # freed by its last flusher
-    assert refused == [True]
+    assert b2.h is None  # freed by its last flusher; close() dropped the handle
+    b2.close()  # a second close is a no-op
+    assert refused == [True, True]
     got.sort()
     assert [g[1] for g in got] == [mh.OK] * 32
     np.testing.assert_array_equal(np.array([g[2] for g in got]), ref.cert_accept[:32])
@@ -535,4 +542,32 @@ def test_unsigned_33_multigrant_certificate_not_accepted(pool4):
         g, st = ver.verify_write2(wb, 4, strict)
         assert st[0] == mh.MSG_FALLBACK
         assert not g.cert_accept[0] and g.cert_reason[0] == mh.REJECT_NO_GRANT
+    ver.close()
+
+
+def test_ten_byte_varint_garbage_is_not_canonical(pool4):
+    """a negative timestamp is a 10-byte varint whose last byte carries
+    bit 63 alone (0x01).  The same value with last byte 0x03 parses identically (bits
+    past 64 are dropped) but is not Grant.toByteArray(): the device fast path must
+    send it to FALLBACK like the oracle, which re-encodes and compares bytes."""
+    ver = _ver(pool4)
+    oid, th = "DEMO_KEY_NEG_TS", "ab" * 64
+    canon = W.encode_grant(oid, -5, th)
+    v = W._varint(-5)
+    assert len(v) == 10 and v[-1] == 0x01
+    bad = canon.replace(b"\x10" + v, b"\x10" + v[:-1] + b"\x03")
+    assert bad != canon and len(bad) == len(canon)
+    ids = W.SERVER_IDS[:4]
+    msgs = []
+    for gb in (canon, bad):
+        ent = [(ids[r], W.encode_multigrant([(oid, gb)], ids[r], "cl", "", [(oid, b"\x00" * 256)])) for r in range(4)]
+        msgs.append(W.encode_write2(ent, [W.encode_operation(2, oid)]))
+    wb = _pack(msgs)
+    wb.expected_hash = np.zeros((2, 128), np.uint8)
+    g, st = ver.verify_write2(wb, 4, True)
+    wids, woff = W.server_id_table(4)
+    o, ost = O.verify_write2(pool4.moduli, wids, woff, wb, 4, True)
+    np.testing.assert_array_equal(st, ost)
+    assert st[0] == mh.MSG_OK and st[1] == mh.MSG_FALLBACK, st
+    np.testing.assert_array_equal(g.cert_reason, o.cert_reason)
     ver.close()
