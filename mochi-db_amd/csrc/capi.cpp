@@ -288,7 +288,7 @@ struct mochi_ctx {
   uint32_t n_ids = 0;
   std::vector<std::string> server_ids;  // host copy for the fallback decoder (w2_host.cpp)
   DevBuf w2_cnt, w2_status, w2_scan, w2_goff, w2_glen, w2_sig, w2_signer, w2_gkey, w2_okey, w2_oflags, w2_sigsrc,
-      w2_mgo, w2_ots, w2_okoff, w2_oklen;
+      w2_mgo, w2_ots, w2_okoff, w2_oklen, w2_same;
   PinnedBuf w2_tot;
   hipEvent_t ev_tot = nullptr;
   // the last host-path call's certificate accept bitmap on the device (a slice
@@ -529,12 +529,12 @@ hipError_t scratch_release(mochi_ctx* c, hipStream_t st) {
 }
 
 int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o, hipStream_t st,
-               const uint32_t* op_out_off = nullptr) {
+               const uint32_t* op_out_off = nullptr, const uint32_t* grant_same = nullptr) {
   const uint32_t N = b->n_grants, C = b->n_certs;
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
   if (slots > 0xFFFFFFF0ull) return fail(MOCHI_EINVAL, "batch too large");
   int rc;
-  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure(sizeof(uint32_t) * 3 * (size_t)N)) ||
+  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure((size_t)N)) ||
       (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
       (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
       (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
@@ -579,8 +579,8 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.total = c->total.as<uint32_t>();
   a.perm = c->perm.as<uint32_t>();
   a.xbuf = c->xbuf.as<uint32_t>();
-  a.lead = c->dedup.as<uint32_t>();
-  a.leaders = a.lead + N;
+  a.rare = c->dedup.as<uint8_t>();
+  a.grant_same = grant_same;
   a.grant_valid_bits = o->grant_valid_bits;
   a.cert_accept_bits = o->cert_accept_bits;
   a.cert_reason = o->cert_reason;
@@ -648,7 +648,7 @@ void par_memcpy(void* dst, const void* src, size_t n) {
 int ensure_scratch(mochi_ctx* c, uint32_t N) {
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
   int rc;
-  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure(sizeof(uint32_t) * 3 * (size_t)N)) ||
+  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure((size_t)N)) ||
       (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
       (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
       (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
@@ -959,7 +959,7 @@ int w2_verify(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, 
       (rc = grow(c->w2_gkey, N, st)) || (rc = grow(c->w2_okey, O, st)) || (rc = grow(c->w2_oflags, O, st)) ||
       (rc = grow(c->w2_sigsrc, 8 * (size_t)N, st)) || (rc = grow(c->w2_mgo, 4 * ((size_t)NM + 1), st)) ||
       (rc = grow(c->w2_ots, 8 * (size_t)O, st)) || (rc = grow(c->w2_okoff, 8 * (size_t)O, st)) ||
-      (rc = grow(c->w2_oklen, 4 * (size_t)O, st)))
+      (rc = grow(c->w2_oklen, 4 * (size_t)O, st)) || (rc = grow(c->w2_same, 4 * (size_t)N, st)))
     return rc;
   if (!decode_only) {  // the verify scratch grows only once the stream has drained
     const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
@@ -980,6 +980,7 @@ int w2_verify(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, 
   a.op_key_off = c->w2_okoff.as<uint64_t>();
   a.op_key_len = c->w2_oklen.as<uint32_t>();
   a.mg_grant_off = c->w2_mgo.as<uint32_t>();
+  a.grant_same = c->w2_same.as<uint32_t>();
   HIP_TRY(mochi::launch_w2_emit(a, st));
   if (decode_only) return MOCHI_OK;
   mochi_batch db;
@@ -1013,7 +1014,7 @@ int w2_verify(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, 
   dv.op_decision = o->op_decision;
   dv.op_g0 = o->op_g0;
   dv.op_ts = o->op_ts;
-  if ((rc = run_device(c, &db, p, &dv, st, op_out_off))) return rc;
+  if ((rc = run_device(c, &db, p, &dv, st, op_out_off, a.grant_same))) return rc;
   HIP_TRY(mochi::launch_w2_fixup(a, o->cert_accept_bits, o->cert_reason, o->cert_fail_op, o->op_decision, o->op_g0,
                                  o->op_ts, st));
   return MOCHI_OK;

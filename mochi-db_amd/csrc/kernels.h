@@ -41,8 +41,8 @@ struct LaunchArgs {
   uint32_t* count;     // [n_keys]
   uint32_t* cursor;    // [n_keys]
   uint32_t* total;     // [kTotalWords]: bucketed slot total, then per-call counters (zeroed by k_bucket_scan)
-  uint32_t* lead;      // [N] grant dedup: the grant whose prep results g takes (null: no dedup)
-  uint32_t* leaders;   // [2N] (leader, certificate grant end)
+  uint8_t* rare;       // [N] grant prep: grants not covered by their certificate's first grants (null: no dedup)
+  const uint32_t* grant_same;  // [N] or null: the wire decoder's byte-equal earlier grant of the certificate
   uint32_t* perm;      // [n_slots]
   uint32_t* xbuf;      // [kL][n_slots]
   // outputs
@@ -67,7 +67,7 @@ struct LaunchArgs {
 };
 
 // LaunchArgs::total words
-enum TotalWord { kTotSlots = 0, kTotPowGroup, kTotFinalGroup, kTotNLeaders, kTotPrepChunk, kTotalWords = 8 };
+enum TotalWord { kTotSlots = 0, kTotPowGroup, kTotFinalGroup, kTotalWords = 4 };
 
 // Stages timed when LaunchArgs::prof_events is set.
 enum ProfStage { kStagePrep = 0, kStageBucket, kStagePow, kStageFinal, kStageTally, kProfStages };

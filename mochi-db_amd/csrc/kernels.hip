@@ -41,104 +41,123 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep(const PrepAr
 }
 
 // ---------------------------------------------------------------------------
-// Grant dedup: the R grants of one op key in an honest certificate are the same
-// bytes (every replica builds the Grant from the same objectId, transaction
-// hash and timestamp, InMemoryDataStore.java:131-140), so each distinct grant
-// of a certificate is parsed and hashed once.  k_grant_dedup (lane =
-// certificate) byte-compares every grant with the first grant of its
-// (certificate, op key slot) -- bytes, not offsets: wire-path grants are
-// separate copies -- and lists the distinct ones (leaders) in certificate
-// order; k_grant_prep_lead parses and hashes each leader and stores the same
-// results for the grants that matched it (PrepOut is a function of the bytes).
+// Grant prep, each distinct grant of a certificate once.  In an honest
+// certificate the R grants of an op key are the same bytes (every replica
+// builds the Grant from the same objectId, transaction hash and timestamp,
+// InMemoryDataStore.java:131-140), and PrepOut is a function of the bytes.
+// k_grant_prep_cert (lane = certificate) preps the first grant of each key slot
+// (up to two slots kept in registers) and stores its results for every later
+// grant of the slot with the same bytes -- compared as bytes (equal offsets
+// suffice; wire-path grants are separate copies, which the decoder may already
+// have matched: `same`), never assumed.  The rest (a grant that differs from
+// its slot's first, a third slot) is flagged and prepped by k_grant_prep_rare.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kDedupMaxGrants = 256;  // larger certificates: every grant its own leader (the slot scan is quadratic)
-
-struct DedupArgs {
-  const uint8_t* blob;
-  const uint64_t* goff;
-  const uint32_t* glen;
+struct PrepCertArgs {
   const uint8_t* grant_key;
   const uint32_t* cert_grant_off;
+  const uint32_t* same;  // [N] or null: an earlier grant of the certificate with the same bytes (the decoder's match)
   uint32_t n_certs;
-  uint32_t* lead;     // [N]: the grant whose prep results grant g takes (g itself for a leader)
-  uint32_t* leaders;  // [2 x n_leaders]: (leader, its certificate's grant end)
-  uint32_t* n_leaders;
+  uint8_t* rare;         // [N]: 1 = prepped by k_grant_prep_rare (preset to 1: a grant outside every certificate too)
 };
 
-__global__ __launch_bounds__(256) void k_grant_dedup(const DedupArgs a) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t g_lo = 0, g_hi = 0;
-  if (c < a.n_certs) {
-    g_lo = a.cert_grant_off[c];
-    g_hi = a.cert_grant_off[c + 1];
-  }
-  const bool small = g_hi - g_lo <= kDedupMaxGrants;
-  uint32_t nl = 0;
-#pragma unroll 1
-  for (uint32_t g = g_lo; g < g_hi; g++) {
-    uint32_t L = g;
-    if (small) {
-      const uint32_t s = a.grant_key[g];
-#pragma unroll 1
-      for (uint32_t q = g_lo; q < g; q++)
-        if (a.grant_key[q] == s) {
-          L = q;  // the slot's first grant (a leader by construction)
-          break;
-        }
-      if (L != g) {
-        const uint32_t lg = a.glen[g];
-        const uint64_t og = a.goff[g], ol = a.goff[L];
-        if (lg != a.glen[L] || (og != ol && !bytes_equal(a.blob + og, a.blob + ol, lg))) L = g;
-      }
-    }
-    a.lead[g] = L;
-    nl += L == g;
-  }
-  // leaders of the wave's certificates, in certificate order, at one atomic per wave
-  const uint32_t lane = __lane_id();
-  uint32_t incl = nl;
+__device__ __forceinline__ void prep_select(PrepOut& o, const PrepOut& a, const PrepOut& b, bool take_a) {
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(incl, d, 64);
-    if (lane >= (uint32_t)d) incl += v;
-  }
-  const uint32_t tot = __shfl(incl, 63, 64);
-  uint32_t base = 0;
-  if (lane == 0 && tot) base = atomicAdd(a.n_leaders, tot);
-  uint32_t k = __shfl(base, 0, 64) + incl - nl;
-#pragma unroll 1
-  for (uint32_t g = g_lo; g < g_hi && nl; g++)
-    if (a.lead[g] == g) {
-      a.leaders[2 * k] = g;
-      a.leaders[2 * k + 1] = g_hi;
-      k++;
-    }
+  for (int q = 0; q < 8; q++) o.h[q] = take_a ? a.h[q] : b.h[q];
+  o.ts = take_a ? a.ts : b.ts;
+  o.hash_rel = take_a ? a.hash_rel : b.hash_rel;
+  o.hash_len = take_a ? a.hash_len : b.hash_len;
+  o.flags = take_a ? a.flags : b.flags;
 }
 
-// Lane = leader, 256-leader chunks taken from a device counter (the blocks run
-// in k_rsa_pow's tail, on CUs that free up at different times).
-__global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_lead(const PrepArgs a, const uint32_t* __restrict__ lead,
-                                                                         const uint32_t* __restrict__ leaders,
-                                                                         const uint32_t* __restrict__ n_leaders,
-                                                                         uint32_t* __restrict__ chunk) {
-  __shared__ uint32_t s_base[2];
-  const uint32_t n = __builtin_amdgcn_readfirstlane(*n_leaders);
-  for (uint32_t it = 0;; it ^= 1) {
-    if (threadIdx.x == 0) s_base[it] = atomicAdd(chunk, blockDim.x);
-    __syncthreads();
-    const uint32_t base = __builtin_amdgcn_readfirstlane(s_base[it]);
-    if (base >= n) break;
-    const uint32_t i = base + threadIdx.x;
-    if (i < n) {
-      const uint32_t L = leaders[2 * i], end = leaders[2 * i + 1];
-      PrepOut o;
-      grant_prep_bytes(a.blob + a.goff[L], a.glen[L], o);
-      grant_prep_store(a, L, o);
+__global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const PrepArgs a, const PrepCertArgs p) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.n_certs) return;
+  const uint32_t g_lo = p.cert_grant_off[c], g_hi = p.cert_grant_off[c + 1];
+  uint32_t s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu, L0 = 0, L1 = 0;  // cached slots and their first grants
+  PrepOut o0, o1;
 #pragma unroll 1
-      for (uint32_t g = L + 1; g < end; g++)
-        if (lead[g] == L) grant_prep_store(a, g, o);
+  for (uint32_t g = g_lo; g < g_hi; g++) {
+    const uint32_t s = p.grant_key[g];
+    const uint32_t hint = p.same ? p.same[g] : g;
+    const bool in0 = s0 != 0xFFFFFFFFu && (s == s0 || hint == L0);
+    const bool in1 = s1 != 0xFFFFFFFFu && (s == s1 || hint == L1);
+    if (in0 || in1) {  // a later grant of a cached slot: its results if the bytes are the same
+      const uint32_t L = in0 ? L0 : L1;
+      const uint64_t og = a.goff[g], ol = a.goff[L];
+      const uint32_t lg = a.glen[g];
+      const bool eq = hint == L || (lg == a.glen[L] && (og == ol || bytes_equal(a.blob + og, a.blob + ol, lg)));
+      if (eq) {
+        PrepOut o;
+        prep_select(o, o0, o1, in0);
+        grant_prep_store(a, g, o);
+      }
+      p.rare[g] = eq ? 0 : 1;
+      continue;
+    }
+    // an uncached slot: g is its first grant unless two slots came before
+    bool first = s1 == 0xFFFFFFFFu;
+    if (!first) {
+      first = true;
+#pragma unroll 1
+      for (uint32_t q = g_lo; q < g; q++)
+        if (p.grant_key[q] == s) {
+          first = false;
+          break;
+        }
+    }
+    if (!first) {
+      p.rare[g] = 1;
+      continue;
+    }
+    PrepOut o;
+    grant_prep_bytes(a.blob + a.goff[g], a.glen[g], o);
+    grant_prep_store(a, g, o);
+    p.rare[g] = 0;
+    if (s0 == 0xFFFFFFFFu) {
+      s0 = s;
+      L0 = g;
+      o0 = o;
+    } else if (s1 == 0xFFFFFFFFu) {
+      s1 = s;
+      L1 = g;
+      o1 = o;
     }
   }
+}
+
+// The flagged grants, compacted per block: each block scans kRareSpan flags
+// (16 per thread, one 16-byte load), queues the flagged ones in LDS and preps
+// them with consecutive lanes -- a few per block, so one prep time per block.
+constexpr uint32_t kRareSpan = 4096;
+
+__global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_rare(const PrepArgs a, const uint8_t* __restrict__ rare) {
+  __shared__ uint32_t q[kRareSpan];
+  __shared__ uint32_t nq;
+  if (threadIdx.x == 0) nq = 0;
+  __syncthreads();
+  const uint32_t g0 = blockIdx.x * kRareSpan + 16 * threadIdx.x;
+  if (g0 < a.n) {
+    uint32_t f[4];
+    if (g0 + 16 <= a.n) {
+      const uint4 v = *(const uint4*)(rare + g0);  // g0 is a multiple of 16: aligned
+      f[0] = v.x, f[1] = v.y, f[2] = v.z, f[3] = v.w;
+    } else {
+      for (int k = 0; k < 4; k++) {
+        f[k] = 0;
+        for (int b = 0; b < 4; b++)
+          if (g0 + 4 * k + b < a.n) f[k] |= (uint32_t)rare[g0 + 4 * k + b] << (8 * b);
+      }
+    }
+    if (f[0] | f[1] | f[2] | f[3]) {
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if ((f[j >> 2] >> (8 * (j & 3))) & 0xFFu) q[atomicAdd(&nq, 1u)] = g0 + j;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = nq;
+#pragma unroll 1
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) grant_prep_one(a, q[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -621,13 +640,12 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   }
   mark(kStagePrep, false, ps);
   if (prep) {
-    if (a.lead && a.leaders && a.cert_grant_off && C && !dedup_off()) {
-      const DedupArgs da{a.blob, a.grant_off, a.grant_len, a.grant_key, a.cert_grant_off, C, a.lead, a.leaders,
-                         a.total + kTotNLeaders};
-      hipLaunchKernelGGL(k_grant_dedup, dim3(cdiv(C, 256)), dim3(256), 0, ps, da);
-      const uint32_t pblocks = cdiv(N, 256) < 4096 ? cdiv(N, 256) : 4096;
-      hipLaunchKernelGGL(k_grant_prep_lead, dim3(pblocks), dim3(256), 0, ps, pa, (const uint32_t*)a.lead,
-                         (const uint32_t*)a.leaders, (const uint32_t*)(a.total + kTotNLeaders), a.total + kTotPrepChunk);
+    if (a.rare && a.cert_grant_off && C && !dedup_off()) {
+      const PrepCertArgs pc{a.grant_key, a.cert_grant_off, a.grant_same, C, a.rare};
+      hipError_t e = hipMemsetAsync(a.rare, 1, N, ps);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_grant_prep_cert, dim3(cdiv(C, 256)), dim3(256), 0, ps, pa, pc);
+      hipLaunchKernelGGL(k_grant_prep_rare, dim3(cdiv(N, kRareSpan)), dim3(256), 0, ps, pa, (const uint8_t*)a.rare);
     } else {
       hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
     }

@@ -59,38 +59,57 @@ __device__ __forceinline__ void grant_prep_one(const PrepArgs& a, uint32_t i) {
   grant_prep_store(a, i, o);
 }
 
-// n bytes at a and at b equal?  Aligned dword loads funnel-shifted into place
-// (v_alignbyte); every word read holds a byte of its string, so nothing past
-// either grant's last byte is touched (the bytes may be a slice of a wire
-// buffer).
+// Bytes [pos, pos + 64) of the `len` bytes at `base` (any alignment) as 16
+// little-endian words (words past len hold garbage: callers mask them).  Like
+// sha256_block_words: 16-byte-aligned dwordx4 loads, each issued only if its 16
+// bytes hold a byte of the string, a per-lane dword rotation by mask selects
+// and a funnel shift -- 4 or 5 loads per 64 bytes instead of 16 + 16 dword loads
+// (every load of a lane gathered from its own cache line).
+__device__ __forceinline__ void window64(const uint8_t* base, uint32_t len, uint32_t pos, uint32_t (&w)[16]) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const uintptr_t addr = (uintptr_t)base + pos;
+  const v4u* a16 = (const v4u*)(addr & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(addr & 15);
+  const int64_t p0 = (int64_t)pos - sh;  // string position of the first loaded byte
+  uint32_t d[20];
+#pragma unroll
+  for (int c = 0; c < 5; c++) {
+    v4u v = {0u, 0u, 0u, 0u};
+    if (p0 + 16 * c < (int64_t)len && (c < 4 || sh != 0)) v = a16[c];
+    d[4 * c] = v.x;
+    d[4 * c + 1] = v.y;
+    d[4 * c + 2] = v.z;
+    d[4 * c + 3] = v.w;
+  }
+  const uint32_t m4 = 0u - ((sh >> 2) & 1u), m8 = 0u - ((sh >> 3) & 1u);
+  uint32_t e1[19], e[17];
+#pragma unroll
+  for (int j = 0; j < 19; j++) e1[j] = (d[j + 1] & m4) | (d[j] & ~m4);
+#pragma unroll
+  for (int j = 0; j < 17; j++) e[j] = (e1[j + 2] & m8) | (e1[j] & ~m8);
+  const uint32_t r = 8 * (sh & 3);
+#pragma unroll
+  for (int t = 0; t < 16; t++) w[t] = __builtin_amdgcn_alignbit(e[t + 1], e[t], r);
+}
+
+// n bytes at a and at b equal?  64 bytes per step (window64); nothing past
+// either string's last byte is read (the bytes may be a slice of a wire buffer).
 __device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
-  const uintptr_t pa = (uintptr_t)a, pb = (uintptr_t)b;
-  const uint32_t* wa = (const uint32_t*)(pa & ~(uintptr_t)3);
-  const uint32_t* wb = (const uint32_t*)(pb & ~(uintptr_t)3);
-  const uint32_t sa = (uint32_t)(pa & 3), sb = (uint32_t)(pb & 3);
-  uint32_t diff = 0, i = 0;
 #pragma unroll 1
-  for (; i + 16 <= n; i += 16) {
-    const uint32_t k = i >> 2;
-    uint32_t xa[5], xb[5];
+  for (uint32_t pos = 0; pos < n; pos += 64) {
+    uint32_t wa[16], wb[16];
+    window64(a, n, pos, wa);
+    window64(b, n, pos, wb);
+    uint32_t diff = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      xa[j] = wa[k + j];
-      xb[j] = wb[k + j];
+    for (int t = 0; t < 16; t++) {
+      const int32_t left = (int32_t)(n - pos) - 4 * t;  // bytes of word t inside the strings
+      const uint32_t m = left >= 4 ? ~0u : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
+      diff |= (wa[t] ^ wb[t]) & m;
     }
-    xa[4] = sa ? wa[k + 4] : 0u;  // holds byte i + 15 when sa > 0
-    xb[4] = sb ? wb[k + 4] : 0u;
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      diff |= __builtin_amdgcn_alignbyte(xa[j + 1], xa[j], sa) ^ __builtin_amdgcn_alignbyte(xb[j + 1], xb[j], sb);
     if (diff) return false;
   }
-#pragma unroll 1
-  for (; i < n; i++) {
-    const uint32_t ia = i + sa, ib = i + sb;
-    diff |= ((wa[ia >> 2] >> (8 * (ia & 3))) ^ (wb[ib >> 2] >> (8 * (ib & 3)))) & 0xFFu;
-  }
-  return diff == 0;
+  return true;
 }
 
 }  // namespace mochi

@@ -47,7 +47,11 @@ namespace {
 // every multiply reads all 16 entries in a fixed order and keeps one with a
 // mask computed in VGPRs (v_cmp / v_cndmask, no branch on the digit), so the
 // addresses, the instruction stream and its timing are the same for every
-// digit (16 x 37 scratch loads per multiply, ~5 % of the signing time).
+// digit.  Cost (measured, round 4): 16 x 37 scratch loads per multiply make
+// the signer memory-bound on its scratch table (PMC: frac_wait_any 0.62) and
+// halved its rate, 5.26e6 -> 2.68e6 signatures/s; the
+// producer side is not the verify path, and constant-time lookups are the
+// point.
 template <int L>
 __device__ __forceinline__ void table_select(uint32_t (&out)[L], const uint32_t (&tbl)[16][L], uint32_t w) {
   uint32_t wv = w;

@@ -53,6 +53,7 @@ struct W2Args {
   uint64_t* op_key_off;
   uint32_t* op_key_len;
   uint32_t* mg_grant_off;    // [n_mgs+1]
+  uint32_t* grant_same;      // [N] or null: an earlier grant of the message with the same bytes (k_w2_mg's match)
 };
 // Device words of one decode's per-batch scratch: 13 arrays of M+1 (counts,
 // CSR offsets, level-1 state) + the certificate-entry list (at most

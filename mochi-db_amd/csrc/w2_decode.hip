@@ -34,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "../../include/mochi_hip.h"
+#include "prep_dev.h"
 #include "proto_dev.h"
 #include "w2.h"
 
@@ -179,13 +180,21 @@ struct Entry {
   uint32_t voff, vlen;  // value (last occurrence; default empty)
   uint32_t nval;
   bool canon;           // Grant value (kind 1): the last value is canonical Grant bytes
+  bool assumed;         // ... taken as canonical without a parse: its bytes equal the reference grant's
+};
+
+// A Grant slice of the message whose validity and canonical form another lane
+// decides (k_w2_mg: the first grant of the message's first MultiGrant); ~0 = none.
+struct RefGrant {
+  uint32_t off = ~0u, len = 0;
 };
 
 // map<string, V> entry; kind 0 = bytes value, 1 = Grant value: validated, and
 // its key and value read as read_entry reads them (last occurrence of each)
-__device__ bool valid_leaf_read(ByteReader& r, uint32_t off, uint32_t len, int kind, Entry& e) {
+__device__ bool valid_leaf_read(ByteReader& r, uint32_t off, uint32_t len, int kind, Entry& e,
+                                const RefGrant ref = RefGrant{}) {
   e.koff = e.klen = e.voff = e.vlen = e.nval = 0;
-  e.canon = false;
+  e.canon = e.assumed = false;
   uint32_t pos = off, end = off + len;
   Fld f;
   int rc;
@@ -197,7 +206,14 @@ __device__ bool valid_leaf_read(ByteReader& r, uint32_t off, uint32_t len, int k
       e.koff = f.off;
       e.klen = f.len;
     } else if (f.field == 2) {
-      if (kind == 1 && !valid_grant_at(r, f.off, f.len, e.canon)) return false;
+      if (kind == 1) {
+        // the same bytes as the reference grant: its lane parses them (an
+        // invalid grant makes the whole message MALFORMED there) and reports
+        // a non-canonical one (kStFirstNC), so only the byte compare runs here
+        e.assumed = ref.off != ~0u && f.len == ref.len && bytes_equal(r.base + f.off, r.base + ref.off, f.len);
+        if (e.assumed) e.canon = true;
+        else if (!valid_grant_at(r, f.off, f.len, e.canon)) return false;
+      }
       e.voff = f.off;
       e.vlen = f.len;
       e.nval++;
@@ -466,6 +482,7 @@ struct W2Out {
   uint64_t* op_key_off;
   uint32_t* op_key_len;
   uint32_t* mg_grant_off;
+  uint32_t* grant_same;  // or null
 };
 
 // Per-message decode state (W2Args::cnt_ce onwards; cnt_o is W2Args::cnt_o).
@@ -598,20 +615,23 @@ struct MGScan {
   uint32_t nge, nse;
   Entry g, sg;               // last grants / grantSignatures entry
   uint32_t sid_off, sid_len;  // MultiGrant.serverId (last)
+  bool first_nc;             // the first grants entry holds one value, parsed and not canonical
 };
 
-__device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan& m) {
+__device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan& m, const RefGrant ref = RefGrant{}) {
   uint32_t pos = off, end = off + len;
   Fld f;
   int rc;
   m.nge = m.nse = 0;
   m.sid_off = m.sid_len = 0;
+  m.first_nc = false;
 #pragma unroll 1
   while ((rc = next_fld(r, pos, end, f)) > 0) {
     if (f.wt != 2) continue;
     if (f.field == 1) {
       m.nge++;
-      if (!valid_leaf_read(r, f.off, f.len, 1, m.g)) return false;
+      if (!valid_leaf_read(r, f.off, f.len, 1, m.g, ref)) return false;
+      if (m.nge == 1) m.first_nc = m.g.nval == 1 && !m.g.canon && !m.g.assumed;
     } else if (f.field >= 2 && f.field <= 4) {
       if (!valid_utf8(r, f.off, f.len)) return false;
       if (f.field == 4) {
@@ -875,8 +895,9 @@ __device__ void walk_mg(ByteReader& r, uint32_t mo, uint32_t ml, uint32_t tx_off
 }
 
 __device__ __forceinline__ void emit_grant(const W2Out& out, uint32_t g, uint64_t msg_off, uint32_t goff, uint32_t glen,
-                                           uint16_t signer, uint32_t sig_off, uint8_t key) {
+                                           uint16_t signer, uint32_t sig_off, uint8_t key, uint32_t same = ~0u) {
   out.grant_off[g] = msg_off + goff;
+  if (out.grant_same) out.grant_same[g] = same != ~0u ? same : g;
   out.grant_len[g] = glen;
   out.signer[g] = signer;
   // the 256 signature bytes are gathered by k_w2_sig (coalesced, 16 lanes per grant)
@@ -954,6 +975,34 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
   }
 }
 
+// The first grant of a MultiGrant value in the reference encoder's layout: its
+// first field a grants entry holding exactly a key and one value (0x0A klen key
+// 0x12 glen grant).  Only the framing is read; anything else: none.
+__device__ RefGrant first_grant(ByteReader& r, uint32_t off, uint32_t len) {
+  RefGrant g;
+  uint32_t pos = off, end = off + len, l1, kl, gl;
+  if (pos >= end || r.at(pos) != 0x0Au) return g;
+  pos++;
+  if (!vlen(r, pos, end, l1)) return g;
+  const uint32_t e1 = pos + l1;
+  if (pos >= e1 || r.at(pos) != 0x0Au) return g;
+  pos++;
+  if (!vlen(r, pos, e1, kl)) return g;
+  pos += kl;
+  if (pos >= e1 || r.at(pos) != 0x12u) return g;
+  pos++;
+  if (!vlen(r, pos, e1, gl) || pos + gl != e1) return g;
+  g.off = pos;
+  g.len = gl;
+  return g;
+}
+
+// Status bits beside kStMal / kStFb (k_w2_mg): a lane took a grant's canonical
+// form from the message's first grant (kStAssume), and that grant is not
+// canonical (kStFirstNC): together they make the message FALLBACK (k_w2_final),
+// as the lane's own parse would have.
+constexpr uint32_t kStAssume = 4u, kStFirstNC = 8u;
+
 // Level 2 (lane = certificate entry; grid-stride over the device-side total).
 // MOCHI_W2_STAMPS (measurement builds only, `make ab VSRC=w2_decode`): per
 // wave, s_memtime ticks spent between the marks of k_w2_mg (dedup, scan,
@@ -1023,6 +1072,10 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
     const uint32_t vo = ce.voff[e], vl = ce.vlen[e];
     uint32_t bits = 0, ng = 0;
     MGScan sc;
+    // the R MultiGrants of an honest certificate carry the same grant bytes:
+    // a grant equal to the first MultiGrant's first grant is parsed by that
+    // entry's lane only
+    const RefGrant ref = e != b0 ? first_grant(r, ce.voff[b0], ce.vlen[b0]) : RefGrant{};
     // the emit record, read by k_w2_emit_mg when ng == 1
     auto rec = [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
       ce.r_goff[e] = go;
@@ -1031,8 +1084,9 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
       ce.r_sk[e] = (uint32_t)sg << 8 | key;
     };
     stp.mark(1);
-    const bool valid = valid_mg_scan(r, vo, vl, sc);
+    const bool valid = valid_mg_scan(r, vo, vl, sc, ref);
     stp.mark(2);
+    if (valid && e == b0 && sc.first_nc) bits |= kStFirstNC;  // the reference grant of this message's other lanes
     if (!valid) {
       bits = kStMal;
     } else if (last == e) {  // this entry's value is the key's final one: it is decoded
@@ -1041,9 +1095,10 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
         // first and last; its signature is the signature entry if that entry's
         // key is the grant's (walk_mg's lookup over one entry)
         const bool canon = sc.g.nval <= 1 && sc.g.canon;  // decided by the validating parse
+        if (canon && sc.g.assumed) bits |= kStAssume;
         stp.mark(3);
         if (!canon) {
-          bits = kStFb;
+          bits |= kStFb;
         } else {
           ng = 1;
           const bool have = sc.nse == 1 && key_eq(r, sc.sg.koff, sc.sg.klen, sc.g.koff, sc.g.klen);
@@ -1052,14 +1107,15 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
           const uint8_t slot = find_key_slot_rec(r, s, m, sc.g.koff, sc.g.klen);
           stp.mark(5);
           rec(sc.g.voff, sc.g.vlen, signer, have && sc.sg.vlen == MOCHI_RSA_BYTES ? sc.sg.voff : ~0u, slot);
+          if (sc.g.assumed) ce.r_sk[e] |= 1u << 31;  // its bytes are the message's first grant's (k_w2_emit_mg)
         }
       } else if (sc.nge > kMaxGrantsPerMG || sc.nse > kMaxSigEntries ||
                  !mg_decode_first(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, ng, rec)) {
-        bits = kStFb;
+        bits |= kStFb;
       }
     }
     ce.last[e] = first ? last : ~0u;
-    ce.ng[e] = bits ? 0u : ng;
+    ce.ng[e] = (bits & (kStMal | kStFb)) ? 0u : ng;
     if (bits) atomicOr(s.st_bits + m, bits);
     stp.mark(6);
   }
@@ -1079,7 +1135,8 @@ __global__ __launch_bounds__(256) void k_w2_final(uint32_t M, const uint32_t* __
     cnt4[M] = make_uint4(0, 0, 0, 0);
     return;
   }
-  const uint32_t bits = s.st_bits[m];
+  uint32_t bits = s.st_bits[m];
+  if ((bits & kStAssume) && (bits & kStFirstNC)) bits |= kStFb;  // a lane's assumed-canonical grant was not
   uint32_t st = (bits & kStMal) ? MOCHI_MSG_MALFORMED : (bits & kStFb) ? MOCHI_MSG_FALLBACK : MOCHI_MSG_OK;
   uint32_t no = s.cnt_o[m], ng = 0, nm = 0;
   if (st == MOCHI_MSG_OK && flags_off && flags_off[m + 1] - flags_off[m] != no) st = MOCHI_MSG_OPS_MISMATCH;
@@ -1131,7 +1188,12 @@ __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ 
     const uint64_t mo = moff[m];
     if (ce.ng[L] == 1) {  // recorded by k_w2_mg
       const uint32_t sk = ce.r_sk[L];
-      emit_grant(out, g, mo, ce.r_goff[L], ce.r_glen[L], (uint16_t)(sk >> 8), ce.r_sig[L], (uint8_t)sk);
+      // the same bytes as the message's first grant -- the first one emitted
+      // (base.x) when the first entry holds its key's final value, one grant
+      const uint32_t b0 = s.ce_base[m];
+      const bool same = (sk >> 31) && L != b0 && ce.last[b0] == b0 && ce.ng[b0] == 1;
+      emit_grant(out, g, mo, ce.r_goff[L], ce.r_glen[L], (uint16_t)(sk >> 8), ce.r_sig[L], (uint8_t)sk,
+                 same ? base.x : ~0u);
       continue;
     }
     ByteReader r;
@@ -1322,7 +1384,7 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
 
 hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
   W2Out o{a.sig_src, a.grant_off, a.grant_len, a.sig, a.signer, a.grant_key, a.op_key, a.op_flags,
-          a.op_object_ts, a.op_key_off, a.op_key_len, a.mg_grant_off};
+          a.op_object_ts, a.op_key_off, a.op_key_len, a.mg_grant_off, a.grant_same};
   const W2Msg s = msg_view(a);
   const CE ce = ce_view(a.ce, a.ce_cap);
   if (a.M)

@@ -2,5 +2,7 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_write2_wire_gpu.py -x -q -m gpu -k "dedup or golden or branch or synthetic or c2 or edge or long or ten_byte or callback or fallback or fuzz" --timeout 300 --timeout-method thread > gpurun_out/t1.log 2>&1 || { tail -30 gpurun_out/t1.log; exit 1; }
 tail -2 gpurun_out/t1.log
+AB_LIBS="mochi-db_amd/libmochi_hip_dyn.so mochi-db_amd/libmochi_hip_fpipe.so mochi-db_amd/libmochi_hip_fsplit.so mochi-db_amd/libmochi_hip_fboth.so" bash scripts/gpu.sh parity || exit 1
 AB_ENVS="MOCHI_NO_DEDUP=1;MOCHI_PREP_SERIAL=1;MOCHI_NO_DEDUP=1 MOCHI_PREP_SERIAL=1" bash scripts/gpu.sh abenv || exit 1
+AB_LIBS="mochi-db_amd/libmochi_hip_fpipe.so mochi-db_amd/libmochi_hip_fsplit.so mochi-db_amd/libmochi_hip_fboth.so" bash scripts/gpu.sh ab || exit 1
 AB_LIBS=mochi-db_amd/libmochi_hip_dyn.so BENCH_ARGS="--shard-sizes" bash scripts/gpu.sh ab

@@ -392,8 +392,8 @@ def test_batcher_callback_reentry(pool4):
                 b2.close()  # deferred: this callback runs on one of b2's flushers
                 # the library refuses a submission after the (deferred) destroy; the
                 # batcher is alive at least until this callback returns
-                rc = b2.lib.mochi_batcher_submit(h, msgs[40], len(msgs[40]), None, 0, hashes[40], b2._cb, 0)
-                if rc == mh.EINVAL:
+                rc2 = b2.lib.mochi_batcher_submit(h, msgs[40], len(msgs[40]), None, 0, hashes[40], b2._cb, 0)
+                if rc2 == mh.EINVAL:
                     refused.append(True)
                 try:
                     b2.submit(msgs[40], hashes[40], lambda *a: None)
