@@ -355,9 +355,12 @@ def main():
             "stage_ms": {"prep_sha256": round(stage_ms[0], 4), "bucket": round(stage_ms[1], 4),
                          "rsa_pow": round(stage_ms[2], 4), "rsa_final": round(stage_ms[3], 4),
                          "tally": round(stage_ms[4], 4),
-                         "note": "prep_sha256 = k_grant_prep on the aux stream, launched "
-                                 "beside k_rsa_pow: its blocks run in pow's tail (serialised before it "
-                                 "with MOCHI_PREP_SERIAL=1)"},
+                         "outside_serial_stages": round(t_max / args.steps * 1e3 - sum(stage_ms[1:]), 4),
+                         "note": "prep_sha256 = k_grant_prep_cert + k_grant_prep_rare on the aux stream, "
+                                 "launched beside k_rsa_pow (its blocks run in pow's tail; serialised before "
+                                 "it with MOCHI_PREP_SERIAL=1): its span ends after pow's; "
+                                 "outside_serial_stages = step - bucket - pow - final - tally"},
+            "prep_dedup": prep_dedup(batch) if rank == 0 else None,
             "c3": c3,
             "shard_sizes": shard_leg,
             "host_path_pcie_inclusive_grants_per_s": hostp["pinned_grants_per_s"] if hostp else None,
@@ -459,6 +462,27 @@ def shard_sizes_leg(args, ver, synth, C_total, R, strict, dev, stream, head_pow_
     return {"rows": rows, "full_pow_ns_per_grant": round(head_ns, 4),
             "note": "rank 0's shard of the C4 stream at each N, on this one GPU (strong scaling: what each rank "
                     "runs); pow_per_grant_vs_full = k_rsa_pow ns/grant at that size / at 16M"}
+
+
+def prep_dedup(batch):
+    """Grants k_grant_prep_cert + k_grant_prep_rare parse and hash:
+    the first grant of each (certificate, key slot) plus every later grant of the
+    slot whose bytes differ from it (in the SoA stream a distinct byte string is
+    stored once per certificate, so equal bytes <=> equal offset and length)."""
+    import numpy as np
+
+    cgo = np.asarray(batch.cert_grant_off, np.int64)
+    n = int(cgo[-1])
+    cert = np.repeat(np.arange(len(cgo) - 1, dtype=np.int64), np.diff(cgo))
+    key = cert * 256 + np.asarray(batch.grant_key[:n], np.int64)
+    _, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    lead = first[inv]
+    off = np.asarray(batch.grant_off[:n], np.uint64)
+    ln = np.asarray(batch.grant_len[:n], np.uint32)
+    rare = int(np.count_nonzero((off != off[lead]) | (ln != ln[lead])))
+    return {"grants": n, "prepped": int(len(first)) + rare, "leaders": int(len(first)), "rare": rare,
+            "ratio": round((len(first) + rare) / max(1, n), 4),
+            "note": "grants parsed + SHA-256'd per step; every other grant takes its slot leader's results"}
 
 
 def host_path(ver, batch, R, strict, reps=3):

@@ -46,11 +46,11 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep(const PrepAr
 // builds the Grant from the same objectId, transaction hash and timestamp,
 // InMemoryDataStore.java:131-140), and PrepOut is a function of the bytes.
 // k_grant_prep_cert (lane = certificate) preps the first grant of each key slot
-// (up to two slots kept in registers) and stores its results for every later
-// grant of the slot with the same bytes -- compared as bytes (equal offsets
-// suffice; wire-path grants are separate copies, which the decoder may already
-// have matched: `same`), never assumed.  The rest (a grant that differs from
-// its slot's first, a third slot) is flagged and prepped by k_grant_prep_rare.
+// (up to two slots) and stores its results for every later grant of the slot
+// with the same bytes -- compared as bytes (equal offsets suffice; wire-path
+// grants are separate copies, which the decoder may already have matched:
+// `same`), never assumed.  The rest (a grant that differs from its slot's
+// first, a third slot) keeps its flag (memset 1) and k_grant_prep_rare preps it.
 // ---------------------------------------------------------------------------
 struct PrepCertArgs {
   const uint8_t* grant_key;
@@ -60,43 +60,20 @@ struct PrepCertArgs {
   uint8_t* rare;         // [N]: 1 = prepped by k_grant_prep_rare (preset to 1: a grant outside every certificate too)
 };
 
-__device__ __forceinline__ void prep_select(PrepOut& o, const PrepOut& a, const PrepOut& b, bool take_a) {
-#pragma unroll
-  for (int q = 0; q < 8; q++) o.h[q] = take_a ? a.h[q] : b.h[q];
-  o.ts = take_a ? a.ts : b.ts;
-  o.hash_rel = take_a ? a.hash_rel : b.hash_rel;
-  o.hash_len = take_a ? a.hash_len : b.hash_len;
-  o.flags = take_a ? a.flags : b.flags;
-}
-
 __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const PrepArgs a, const PrepCertArgs p) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= p.n_certs) return;
   const uint32_t g_lo = p.cert_grant_off[c], g_hi = p.cert_grant_off[c + 1];
-  uint32_t s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu, L0 = 0, L1 = 0;  // cached slots and their first grants
-  PrepOut o0, o1;
+  uint64_t seen = 0;  // key slots < 64 whose first grant came already (others: a scan back)
+  uint32_t leaders = 0;
 #pragma unroll 1
   for (uint32_t g = g_lo; g < g_hi; g++) {
     const uint32_t s = p.grant_key[g];
-    const uint32_t hint = p.same ? p.same[g] : g;
-    const bool in0 = s0 != 0xFFFFFFFFu && (s == s0 || hint == L0);
-    const bool in1 = s1 != 0xFFFFFFFFu && (s == s1 || hint == L1);
-    if (in0 || in1) {  // a later grant of a cached slot: its results if the bytes are the same
-      const uint32_t L = in0 ? L0 : L1;
-      const uint64_t og = a.goff[g], ol = a.goff[L];
-      const uint32_t lg = a.glen[g];
-      const bool eq = hint == L || (lg == a.glen[L] && (og == ol || bytes_equal(a.blob + og, a.blob + ol, lg)));
-      if (eq) {
-        PrepOut o;
-        prep_select(o, o0, o1, in0);
-        grant_prep_store(a, g, o);
-      }
-      p.rare[g] = eq ? 0 : 1;
-      continue;
-    }
-    // an uncached slot: g is its first grant unless two slots came before
-    bool first = s1 == 0xFFFFFFFFu;
-    if (!first) {
+    bool first;
+    if (s < 64) {
+      first = !((seen >> s) & 1);
+      seen |= 1ull << s;
+    } else {
       first = true;
 #pragma unroll 1
       for (uint32_t q = g_lo; q < g; q++)
@@ -105,22 +82,27 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const P
           break;
         }
     }
-    if (!first) {
-      p.rare[g] = 1;
-      continue;
+    if (!first) continue;  // decided in its slot's first grant's pass
+    if (leaders++ == 2) {  // a third slot: its grants are left to k_grant_prep_rare (rare stays 1)
+      break;
     }
+    // g leads its slot: prep it, then hand its results to every later grant of the
+    // slot with the same bytes; a grant that differs stays flagged
     PrepOut o;
-    grant_prep_bytes(a.blob + a.goff[g], a.glen[g], o);
+    const uint64_t og = a.goff[g];
+    const uint32_t lg = a.glen[g];
+    grant_prep_bytes(a.blob + og, lg, o);
     grant_prep_store(a, g, o);
     p.rare[g] = 0;
-    if (s0 == 0xFFFFFFFFu) {
-      s0 = s;
-      L0 = g;
-      o0 = o;
-    } else if (s1 == 0xFFFFFFFFu) {
-      s1 = s;
-      L1 = g;
-      o1 = o;
+#pragma unroll 1
+    for (uint32_t h = g + 1; h < g_hi; h++) {
+      if (p.grant_key[h] != s) continue;
+      const uint64_t oh = a.goff[h];
+      const bool eq = (p.same && p.same[h] == g) ||
+                      (a.glen[h] == lg && (oh == og || bytes_equal(a.blob + oh, a.blob + og, lg)));
+      if (!eq) continue;
+      grant_prep_store(a, h, o);
+      p.rare[h] = 0;
     }
   }
 }
