@@ -28,13 +28,6 @@
 #include "fold_dev.h"
 #include "rsa_common.h"
 
-// MOCHI_FINAL_PREFETCH (A/B): each item's operands (z, s, digest) are loaded
-// while the previous item's fold runs -- at one wave per SIMD nothing else
-// covers the HBM latency of a half-group's loads
-#ifndef MOCHI_FINAL_PREFETCH
-#define MOCHI_FINAL_PREFETCH 0
-#endif
-
 namespace mochi {
 namespace {
 
@@ -42,21 +35,17 @@ namespace {
 struct FinalOps {
   uint4 sr[16];
   uint32_t z[kL];
-  uint32_t hw[8];  // digest words (MOCHI_FINAL_PREFETCH: loaded with the rest)
   uint32_t g;
 };
 
-__device__ __forceinline__ void final_load_sig(uint32_t slot, uint32_t g_lead, const uint32_t* __restrict__ perm,
-                                               uint32_t n_slots, const uint8_t* __restrict__ sig, FinalOps& o) {
+__device__ __forceinline__ void final_load(uint32_t slot, uint32_t g_lead, const uint32_t* __restrict__ perm,
+                                           uint32_t n_slots, const uint8_t* __restrict__ sig,
+                                           const uint32_t* __restrict__ zin, FinalOps& o) {
   o.g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
   const uint32_t gg = o.g != 0xFFFFFFFFu ? o.g : g_lead;  // inactive lanes shadow the lead grant
   const uint4* s128 = (const uint4*)(sig + (size_t)gg * MOCHI_RSA_BYTES);
 #pragma unroll
   for (int q = 0; q < 16; q++) o.sr[q] = s128[q];
-}
-
-__device__ __forceinline__ void final_load_z(uint32_t slot, uint32_t n_slots, const uint32_t* __restrict__ zin,
-                                             FinalOps& o) {
   // z limb j of this slot: a wave-uniform limb base (SGPRs) + the lane's byte
   // offset (one VGPR), so no 64-bit address per limb stays live.  Every slot
   // of a non-empty group is < n_slots (buckets end 512-aligned inside it).
@@ -71,32 +60,14 @@ __device__ __forceinline__ void final_load_z(uint32_t slot, uint32_t n_slots, co
   }
 }
 
-__device__ __forceinline__ void final_load(uint32_t slot, uint32_t g_lead, const uint32_t* __restrict__ perm,
-                                           uint32_t n_slots, const uint8_t* __restrict__ sig,
-                                           const uint32_t* __restrict__ zin, FinalOps& o) {
-  final_load_sig(slot, g_lead, perm, n_slots, sig, o);
-  final_load_z(slot, n_slots, zin, o);
-}
-
-__device__ __forceinline__ void final_load_digest(uint32_t g_lead, const uint32_t* __restrict__ digest, uint32_t n_grants,
-                                                  FinalOps& o) {
-  const uint32_t gg = o.g != 0xFFFFFFFFu ? o.g : g_lead;
-#pragma unroll
-  for (int i = 0; i < 8; i++) o.hw[i] = digest[(size_t)(7 - i) * n_grants + gg];
-}
-
 // One wave's worth of grants from their loaded operands.
-template <bool PREFETCH = false, typename AfterProduct>
 __device__ __forceinline__ void final_slot(FinalOps& o, uint32_t key, uint32_t g_lead,
                                            const KeyEntry* __restrict__ keys, const FoldKey* __restrict__ fold,
                                            const uint32_t* __restrict__ digest, uint32_t n_grants,
-                                           uint8_t* __restrict__ flags, const v4i* w, AfterProduct&& after_product) {
+                                           uint8_t* __restrict__ flags, const v4i* w) {
   const uint32_t g = o.g;
   const bool active = g != 0xFFFFFFFFu;
-  if (__ballot(active) == 0) {  // this wave's part of the group is padding
-    after_product();                // (the next item's loads are still this wave's to issue)
-    return;
-  }
+  if (__ballot(active) == 0) return;  // this wave's part of the group is padding
   const uint32_t gg = active ? g : g_lead;  // inactive lanes shadow the lead grant (never stored)
   const KeyEntry* ke = keys + key;
   const cptr n = as_const(ke->n);
@@ -122,13 +93,12 @@ __device__ __forceinline__ void final_slot(FinalOps& o, uint32_t key, uint32_t g
   // ---- t = z * s: one level of Karatsuba (kara_dev.h), t_hi biased ----
   uint32_t t[2 * kL];
   kara_product(x, sv, t);
-  after_product();  // (PREFETCH: the next item's loads, issued before the fold)
   // digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
   uint32_t hl[kHL];
   {
     uint32_t hw[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) hw[i] = PREFETCH ? o.hw[i] : digest[(size_t)(7 - i) * n_grants + gg];
+    for (int i = 0; i < 8; i++) hw[i] = digest[(size_t)(7 - i) * n_grants + gg];
 #pragma unroll
     for (int j = 0; j < kHL; j++) {
       const int bit = j * kLimbBits, wi = bit >> 5, sh = bit & 31;
@@ -169,7 +139,6 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
                                                        const uint32_t* __restrict__ digest, uint32_t n_grants,
                                                        uint8_t* __restrict__ flags) {
   __shared__ v4i w[kFoldImgBytes / 16];
-#if !MOCHI_FINAL_PREFETCH
   for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
     // (the next half's operands loaded while this half computes -- into AGPRs,
     // 445 registers, or both halves up front, 483 -- measured 10 % and 18 %
@@ -178,59 +147,9 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
     for (uint32_t h = 0; h < kBucketAlign; h += 256) {
       FinalOps o;
       final_load(base + h + threadIdx.x, g_lead, perm, n_slots, sig, zin, o);
-      final_slot(o, key, g_lead, keys, fold, digest, n_grants, flags, w, [] {});
+      final_slot(o, key, g_lead, keys, fold, digest, n_grants, flags, w);
     }
   });
-#else
-  // items = (group, half) of the block's contiguous range; the next non-empty
-  // item's operands are loaded after this item's product, so their latency
-  // runs under its fold
-  const uint32_t n_groups = (n_slots + kBucketAlign - 1) / kBucketAlign;
-  const uint32_t i_begin = 2 * (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
-  const uint32_t i_end = 2 * (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
-  auto lead_of = [&](uint32_t i) { return __builtin_amdgcn_readfirstlane(perm[(i >> 1) * kBucketAlign]); };
-  auto next_item = [&](uint32_t i) {  // the first item >= i of a non-empty group
-#pragma unroll 1
-    while (i < i_end && lead_of(i) == 0xFFFFFFFFu) i = (i | 1) + 1;
-    return i;
-  };
-  uint32_t i = next_item(i_begin);
-  if (i >= i_end) return;
-  uint32_t cur_key = 0xFFFFFFFFu;
-  FinalOps o;
-  uint32_t g_lead = lead_of(i);
-  final_load((i >> 1) * kBucketAlign + (i & 1) * 256 + threadIdx.x, g_lead, perm, n_slots, sig, zin, o);
-  final_load_digest(g_lead, digest, n_grants, o);
-#pragma unroll 1
-  while (true) {
-    const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)signer[g_lead]);
-    if (key != cur_key) {
-      __syncthreads();  // the old image is no longer read
-      const v4i* src = (const v4i*)fold[key].img;
-      for (uint32_t k = threadIdx.x; k < kFoldImgBytes / 16; k += blockDim.x) w[k] = src[k];
-      __syncthreads();
-      cur_key = key;
-    }
-    const uint32_t inext = next_item(i + 1);
-    const uint32_t lead_next = inext < i_end ? lead_of(inext) : 0u;
-    FinalOps nx;
-    const uint32_t nslot = (inext >> 1) * kBucketAlign + (inext & 1) * 256 + threadIdx.x;
-    final_slot<true>(o, key, g_lead, keys, fold, digest, n_grants, flags, w, [&] {
-      if (inext < i_end) {
-        if (MOCHI_FINAL_PREFETCH != 3) final_load_sig(nslot, lead_next, perm, n_slots, sig, nx);
-        else nx.g = nslot < n_slots ? perm[nslot] : 0xFFFFFFFFu;
-        if (MOCHI_FINAL_PREFETCH != 2) final_load_z(nslot, n_slots, zin, nx);
-        final_load_digest(lead_next, digest, n_grants, nx);
-      }
-    });
-    if (inext >= i_end) break;
-    if (MOCHI_FINAL_PREFETCH == 2) final_load_z(nslot, n_slots, zin, nx);
-    if (MOCHI_FINAL_PREFETCH == 3) final_load_sig(nslot, lead_next, perm, n_slots, sig, nx);
-    o = nx;
-    i = inext;
-    g_lead = lead_next;
-  }
-#endif
 }
 
 }  // namespace

@@ -52,14 +52,6 @@
 #ifndef MOCHI_POW_DYN
 #define MOCHI_POW_DYN 1
 #endif
-// MOCHI_POW_PIPE: groups back to back, no half-empty phase per group (below);
-// needs the device counter
-#ifndef MOCHI_POW_PIPE
-#define MOCHI_POW_PIPE 0
-#endif
-#if MOCHI_POW_PIPE && !MOCHI_POW_DYN
-#error "MOCHI_POW_PIPE takes its groups from the device counter (MOCHI_POW_DYN)"
-#endif
 namespace mochi {
 #if MOCHI_POW_STAMPS
 __device__ unsigned long long g_pow_stamps[4096][5];
@@ -105,107 +97,6 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
   __shared__ v4i w[kFoldImgBytes / 16];
   Stamps st;
   const uint64_t t_begin = stamp();
-#if MOCHI_POW_PIPE
-  // Groups back to back, without the half-empty phase at each end: a lead wave
-  // (0-3) starts group j (load, x^2_0) in the very phase its lag partner folds
-  // the last squaring of group j-1, so per group 32 phases instead of 33 -- one
-  // half-empty phase at the start of the launch and one at its end.  Only when
-  // the key changes (once per bucket boundary) does the pipeline drain for the
-  // restage: the image must not change under the old group's last fold (a
-  // restage inside the squaring loop, right after that shared phase, spilled
-  // ~200 VGPRs).  Groups come from the device counter, fetched one group ahead
-  // by thread 0 into a 4-entry ring in LDS.
-  const bool lag = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
-  const uint32_t n_groups = (a.n_slots + kBucketAlign - 1) / kBucketAlign;
-  __shared__ uint32_t s_grp[4];
-  // the next non-empty group (buckets are padded only at their tail, so a group
-  // whose first slot is empty is all padding: they come last)
-  auto fetch = [&]() -> uint32_t {
-    const uint32_t gi = atomicAdd(a.ctr, 1u);
-    return gi < n_groups && a.perm[gi * kBucketAlign] != 0xFFFFFFFFu ? gi : 0xFFFFFFFFu;
-  };
-  if (threadIdx.x == 0) s_grp[0] = fetch();
-  __syncthreads();
-  uint32_t gcur = __builtin_amdgcn_readfirstlane(s_grp[0]);
-  if (gcur == 0xFFFFFFFFu) return;  // block-uniform: no barrier is left waiting
-  auto key_of = [&](uint32_t grp) {
-    return __builtin_amdgcn_readfirstlane((uint32_t)a.signer[__builtin_amdgcn_readfirstlane(a.perm[grp * kBucketAlign])]);
-  };
-  auto stage = [&](uint32_t key) {
-    const v4i* src = (const v4i*)a.fold[key].img;
-#pragma unroll 1
-    for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
-  };
-  uint32_t cur_key = key_of(gcur);
-  stage(cur_key);
-  __syncthreads();
-  if (lag) phase_barrier();  // phase 0: the lead squares first
-#pragma unroll 1
-  for (uint32_t j = 0;; j++) {
-    if (j > 0) gcur = __builtin_amdgcn_readfirstlane(s_grp[j & 3]);
-    if (gcur == 0xFFFFFFFFu) break;
-    if (threadIdx.x == 0) s_grp[(j + 1) & 3] = fetch();  // read by all after at least one barrier
-    const uint32_t base = gcur * kBucketAlign;
-    const uint32_t g_lead = __builtin_amdgcn_readfirstlane(a.perm[base]);
-    const uint32_t key = key_of(gcur);
-    const bool restage = key != cur_key;  // (the lag waves restaged at the end of group j-1)
-    const uint32_t slot = base + threadIdx.x;
-    const uint32_t g = slot < a.n_slots ? a.perm[slot] : 0xFFFFFFFFu;
-    const bool active = g != 0xFFFFFFFFu;
-    if (!lag && restage) {  // a new key: drain -- idle while the partner folds the old group's last squaring
-      phase_barrier();
-      stage(key);
-      phase_barrier();
-    }
-    if (__ballot(active) == 0) {  // this wave's quarter of the group is padding: only the barriers
-#pragma unroll 1
-      for (int i = 0; i < 32; i++) phase_barrier();
-    } else {
-      uint32_t x[kL];
-      {
-        uint32_t wd[64];
-        load_sig_words(a.sig, active ? g : g_lead, wd);  // inactive lanes shadow the lead grant (never stored)
-        words_to_limbs(wd, x);
-      }
-      const cptr c = as_const(a.fold[key].cadd);
-#pragma unroll 1
-      for (int it = 0; it < 16; it++) {
-        cptr ci = c;
-        asm volatile("" : "+s"(ci));  // keep the 74 cadd loads inside the loop (SGPR pressure if hoisted)
-        uint32_t t[2 * kL];
-        const uint64_t t0 = stamp();
-        kara_square(x, t);  // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
-        const uint64_t t1 = stamp();
-        phase_barrier();
-        __builtin_amdgcn_s_setprio(1);
-        const uint64_t t2 = stamp();
-        fold_reduce<false, true>(t, x, w + (threadIdx.x & 63), ci, nullptr);
-        const uint64_t t3 = stamp();
-        __builtin_amdgcn_s_setprio(0);
-        phase_barrier();
-        st.x2 += t1 - t0;
-        st.fold += t3 - t2;
-        st.n++;
-      }
-      if (active) {
-#pragma unroll
-        for (int q = 0; q < kL; q++) a.zout[(size_t)q * a.n_slots + slot] = x[q];
-      }
-    }
-    cur_key = key;
-    if (lag) {  // the next group takes a new key: restage with the lead (which idled this phase), then
-                // idle while it squares first
-      const uint32_t gn = __builtin_amdgcn_readfirstlane(s_grp[(j + 1) & 3]);
-      if (gn != 0xFFFFFFFFu && key_of(gn) != key) {
-        stage(key_of(gn));
-        phase_barrier();
-        phase_barrier();
-      }
-    }
-  }
-  if (!lag) phase_barrier();  // the last phase: the partner folds its last squaring
-#else
-  {
 
   // waves 4-7 run one phase behind.  Read through readfirstlane so the compiler
   // KNOWS it is wave-uniform: the barriers below sit under `if (lag)`, and a
@@ -283,8 +174,6 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
     }
     if (!lag) phase_barrier();  // phase 32: the partner folds its last squaring
   }
-  }
-#endif
 #if MOCHI_POW_STAMPS
   const uint64_t t_end = stamp();
   const uint32_t wv = blockIdx.x * 8 + (threadIdx.x >> 6);
