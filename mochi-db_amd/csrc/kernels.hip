@@ -267,9 +267,17 @@ __device__ __forceinline__ void load128(const uint8_t* p, uint32_t (&w)[32]) {
   for (int i = 0; i < 32; i++) w[i] = (uint32_t)((((uint64_t)raw[i + 1] << 32) | raw[i]) >> (8 * sh));
 }
 
+// g0's transactionHash == the expected hash: two 64-byte windows per side
+// (bytes_equal, prep_dev.h: 16-byte-aligned dwordx4 loads) instead of load128's
+// 33 dword loads per side -- the tally's lane reads its own cache lines, so the
+// number of load instructions is what its time follows
+#ifndef MOCHI_TALLY_LOAD128
+#define MOCHI_TALLY_LOAD128 0  // A/B: the dword-load compare
+#endif
 __device__ bool hash_matches(const uint8_t* __restrict__ blob, uint64_t off, uint32_t len,
                              const uint8_t* __restrict__ expected) {
   if (len != MOCHI_TXN_HASH_BYTES) return false;
+#if MOCHI_TALLY_LOAD128
   uint32_t a[32], e[32];
   load128(blob + off, a);
   load128(expected, e);
@@ -277,6 +285,9 @@ __device__ bool hash_matches(const uint8_t* __restrict__ blob, uint64_t off, uin
 #pragma unroll
   for (int q = 0; q < 32; q++) diff |= a[q] ^ e[q];
   return diff == 0;
+#else
+  return bytes_equal(blob + off, expected, MOCHI_TXN_HASH_BYTES);
+#endif
 }
 
 // Everything k_tally reads, by value (one kernel argument block).

@@ -31,7 +31,95 @@ struct PrepOut {
   uint8_t flags;
 };
 
+// 16 bytes at p + pos (any alignment) as 4 little-endian words; bytes past l
+// are garbage.  One or two 16-byte-aligned dwordx4 loads, each only if it holds
+// a byte of the string, then a dword rotation by mask selects and a funnel.
+__device__ __forceinline__ void window16(const uint8_t* p, uint32_t l, uint32_t pos, uint32_t (&w)[4]) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const uintptr_t addr = (uintptr_t)p + pos;
+  const v4u* a16 = (const v4u*)(addr & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(addr & 15);
+  const v4u c0 = a16[0];  // holds byte pos (< l)
+  v4u c1 = {0u, 0u, 0u, 0u};
+  if (sh != 0 && pos - sh + 16 < l) c1 = a16[1];
+  const uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const uint32_t m4 = 0u - ((sh >> 2) & 1u), m8 = 0u - ((sh >> 3) & 1u);
+  uint32_t e1[7], e[5];
+#pragma unroll
+  for (int j = 0; j < 7; j++) e1[j] = (d[j + 1] & m4) | (d[j] & ~m4);
+#pragma unroll
+  for (int j = 0; j < 5; j++) e[j] = (e1[j + 2] & m8) | (e1[j] & ~m8);
+  const uint32_t r = 8 * (sh & 3);
+#pragma unroll
+  for (int t = 0; t < 4; t++) w[t] = __builtin_amdgcn_alignbit(e[t + 1], e[t], r);
+}
+
+// The common Grant shape, as protobuf-java writes it (fields in number order,
+// MochiProtocol.java:7556-7574): 0x0A L objectId 0x10 ts 0x22 H transactionHash,
+// L < 128, ts a varint of at most 5 bytes, nothing after the hash.  Its header
+// comes from two 16-byte windows (at 0 and at the timestamp's tag), and its two
+// strings are UTF-8 (valid_utf8's verdict) exactly when they are ASCII: the
+// SHA-256 message words count the bytes with their high bit set, and that
+// count must be the header's own (varint continuation bytes) plus the
+// padding's.  Same outputs as parse_grant for every grant it accepts; false
+// (the generic parse decides) for any other shape or a non-ASCII string.
+// No per-byte loads: the parse's word-by-word reads and the UTF-8 windows were
+// most of the prep's memory requests (lane = certificate: every lane's grant
+// sits in its own cache lines).
+__device__ __forceinline__ bool grant_prep_fast(const uint8_t* p, uint32_t l, PrepOut& o) {
+  if (l < 8) return false;
+  uint32_t w0[4];
+  window16(p, l, 0, w0);
+  const uint32_t L = (w0[0] >> 8) & 0xFFu;
+  if ((w0[0] & 0xFFu) != 0x0Au || L >= 0x80u) return false;
+  const uint32_t q = 2 + L;  // the timestamp's tag
+  if (q + 4 > l) return false;
+  uint32_t hw[4];
+  window16(p, l, q, hw);
+  const uint64_t lo = ((uint64_t)hw[1] << 32) | hw[0], hi = ((uint64_t)hw[3] << 32) | hw[2];
+  auto byte = [&](uint32_t k) -> uint32_t {  // k < 16, relative to q
+    return (uint32_t)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xFFu);
+  };
+  if (byte(0) != 0x10u) return false;
+  uint64_t ts = 0;
+  uint32_t k = 1, hib_hdr = 0;
+  bool end = false;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    if (!end) {
+      const uint32_t c = byte(k++);
+      ts |= (uint64_t)(c & 0x7Fu) << (7 * i);
+      end = c < 0x80u;
+      hib_hdr += c >> 7;
+    }
+  }
+  if (!end || byte(k) != 0x22u) return false;
+  const uint32_t c1 = byte(k + 1), c2 = byte(k + 2);
+  uint32_t hl, hp;
+  if (c1 < 0x80u) {
+    hl = c1;
+    hp = q + k + 2;
+  } else if (c2 < 0x80u) {
+    hl = (c1 & 0x7Fu) | (c2 << 7);
+    hp = q + k + 3;
+    hib_hdr += 1;
+  } else {
+    return false;
+  }
+  if (hp > l || hl != l - hp) return false;  // the hash ends the grant
+  uint32_t hib = 0;
+  sha256(p, l, o.h, &hib);
+  const uint32_t bits = 8 * l;  // the padding: 0x80, then the 64-bit bit length (its low two bytes here)
+  if (hib != hib_hdr + 1 + ((bits >> 15) & 1u) + ((bits >> 7) & 1u) + ((bits >> 23) & 1u)) return false;
+  o.ts = (int64_t)ts;
+  o.hash_rel = hp;
+  o.hash_len = hl;
+  o.flags = MOCHI_GRANT_PARSED;
+  return true;
+}
+
 __device__ __forceinline__ void grant_prep_bytes(const uint8_t* p, uint32_t l, PrepOut& o) {
+  if (grant_prep_fast(p, l, o)) return;
   ByteReader r;
   r.init(p, l);
   int64_t ts = 0;

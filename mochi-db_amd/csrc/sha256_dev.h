@@ -61,8 +61,11 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[
 // base & 15 is the same for every block), a funnel shift and a byte swap.
 // Words at or past the end take the padding: data bytes, 0x80, zeros, and
 // the 64-bit bit length (len < 2^29) in the last two words of the last block.
+// hib (optional): += the bytes with their high bit set among the 64 (padding
+// included: the 0x80 byte and the bit length count too) -- the grant prep's
+// ASCII check rides on these words (prep_dev.h grant_prep_fast)
 __device__ __forceinline__ void sha256_block_words(const uint8_t* base, uint32_t len, uint32_t blk, uint32_t total,
-                                                   uint32_t (&w)[16]) {
+                                                   uint32_t (&w)[16], uint32_t* hib = nullptr) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const uintptr_t addr = (uintptr_t)base + 64u * blk;
   const v4u* a16 = (const v4u*)(addr & ~(uintptr_t)15);
@@ -107,10 +110,11 @@ __device__ __forceinline__ void sha256_block_words(const uint8_t* base, uint32_t
       }
     }
     w[t] = v;
+    if (hib) *hib = __builtin_popcount(v & 0x80808080u) + *hib;  // v_bcnt_u32_b32 with its add
   }
 }
 
-__device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8]) {
+__device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8], uint32_t* hib = nullptr) {
   h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
   h[4] = 0x510e527f; h[5] = 0x9b05688c; h[6] = 0x1f83d9ab; h[7] = 0x5be0cd19;
   const uint32_t nblocks = (len + 9 + 63) >> 6;
@@ -118,7 +122,7 @@ __device__ inline void sha256(const uint8_t* base, uint32_t len, uint32_t (&h)[8
 #pragma unroll 1
   for (uint32_t blk = 0; blk < nblocks; blk++) {
     uint32_t w[16];
-    sha256_block_words(base, len, blk, total, w);
+    sha256_block_words(base, len, blk, total, w, hib);
     sha256_compress(h, w);
   }
 }

@@ -522,3 +522,66 @@ def test_grant_dedup_large_certificate(pool4, ver4):
     g = ver4.verify(b, 4, True)
     o = O.verify_batch(pool4.moduli, b, 4, True, 2)
     assert_same(g, o)
+
+
+def test_grant_prep_fast_path_shapes(pool4, ver4):
+    """prep_dev.h grant_prep_fast takes the common Grant shape (0x0A L objectId 0x10 ts
+    0x22 H hash, ASCII strings) from two 16-byte windows and checks the strings ASCII
+    on the SHA-256 words; every other shape goes to the generic parse.  Shapes at and
+    around its edges -- both sides of each bound -- give the oracle's flags,
+    timestamps and verdicts."""
+    pems = W.load_keys(4)
+    th = W.txn_hash_hex(11)
+    v = W._varint
+
+    def g(oid: bytes, ts_bytes: bytes, hash_b: bytes, tail: bytes = b"", hlen: bytes = None) -> bytes:
+        hl = v(len(hash_b)) if hlen is None else hlen
+        return b"\x0a" + v(len(oid)) + oid + b"\x10" + ts_bytes + b"\x22" + hl + hash_b + tail
+
+    H = th.encode()
+    shapes = [
+        g(b"K", v(1000), H),                        # the common shape
+        g(b"", v(5), H),                            # empty objectId
+        g(b"K" * 127, v(7), H),                     # L = 127 (one-byte length)
+        g(b"K" * 128, v(7), H),                     # L = 128: generic
+        g(b"K", v(0), H),                           # explicit zero timestamp
+        g(b"K", v(2 ** 35 - 1), H),                 # 5-byte varint
+        g(b"K", v(2 ** 35), H),                     # 6-byte varint: generic
+        g(b"K", v(2 ** 63), H),                     # 10-byte varint: generic
+        g(b"K", v(9), H[:127]),                     # 127-byte hash (one-byte length)
+        g(b"K", v(9), b"h" * 200),                  # 2-byte hash length
+        g(b"K", v(9), b""),                         # empty hash
+        g(b"K", v(9), H, tail=b"\x28\x01"),         # a status after the hash: generic
+        g("café".encode(), v(9), H),           # non-ASCII objectId (valid UTF-8): generic
+        g(b"K", v(9), H[:-2] + "é".encode()),  # non-ASCII hash: generic
+        g(b"K\xff", v(9), H),                       # invalid UTF-8 objectId: malformed
+        g(b"K", v(9), H[:-1] + b"\x80"),            # invalid UTF-8 hash: malformed
+        g(b"K", v(9), H)[:-1],                      # truncated: malformed
+        g(b"K", b"\x80\x80\x80\x80\x80\x01", H),    # non-minimal 6-byte varint: generic
+        g(b"K", b"\x85\x00", H),                    # non-minimal 2-byte varint (value 5): valid
+        g(b"K", v(9), H, hlen=b"\x80\x01"[:1] + b"\x81"),  # hash length varint 3 bytes long: malformed
+        b"\x10\x05" + g(b"K", v(9), H)[0:0] + b"\x0a\x01K\x22" + v(len(H)) + H,  # fields out of order
+        b"\x0a\x01K\x18\x01\x22" + v(len(H)) + H,   # configstamp instead of a timestamp: generic
+    ]
+    n = len(shapes)
+    blob = bytearray(b"\x00")
+    offs = []
+    for i, gb in enumerate(shapes):
+        blob += b"\x55" * (i % 5)
+        offs.append(len(blob))
+        blob += gb
+    sigs = [O.rsa_sign(pems[i % 4], gb) for i, gb in enumerate(shapes)]
+    b = mh.Batch(grant_bytes=np.frombuffer(bytes(blob), np.uint8).copy(), grant_off=np.array(offs, np.uint64),
+                 grant_len=np.array([len(x) for x in shapes], np.uint32),
+                 sig=np.frombuffer(b"".join(sigs), np.uint8).reshape(n, 256).copy(),
+                 signer=np.array([i % 4 for i in range(n)], np.uint16), grant_key=np.zeros(n, np.uint8),
+                 cert_grant_off=np.arange(n + 1, dtype=np.uint32), cert_op_off=np.arange(n + 1, dtype=np.uint32),
+                 op_key=np.zeros(n, np.uint8), op_flags=np.full(n, 3, np.uint8),
+                 expected_hash=np.stack([np.frombuffer(H, np.uint8)] * n))
+    for strict in (True, False):
+        gv = ver4.verify(b, 4, strict)
+        o = O.verify_batch(pool4.moduli, b, 4, strict, 2)
+        assert_same(gv, o, f"strict={strict}")
+    assert (gv.grant_flags & 1).all()  # every signature valid: only the parse differs
+    assert not (gv.grant_flags[[14, 15, 16]] & mh.GRANT_PARSED).any()
+    assert (gv.grant_flags[[0, 1, 2, 3, 5, 6, 12, 13, 18]] & mh.GRANT_PARSED).all()
