@@ -60,51 +60,119 @@ struct PrepCertArgs {
   uint8_t* rare;         // [N]: 1 = prepped by k_grant_prep_rare (preset to 1: a grant outside every certificate too)
 };
 
+// The block's first-slot results go out through LDS: each lane puts its
+// leader's results in `lo` and marks the leader and its byte-equal grants in
+// `ref`; then the block stores them grant by grant (consecutive lanes,
+// consecutive grants), not lane = certificate at a 4-grant stride (PMC: 2.58 GB
+// written for 0.86 GB of results that way).  A block whose certificates hold
+// more than kPrepBlockGrants grants, and second slots, store directly.
+constexpr uint32_t kPrepBlockGrants = 2048;
+#ifndef MOCHI_PREP_LDS_STORE
+#define MOCHI_PREP_LDS_STORE 1  // A/B
+#endif
+
+struct PrepOutLds {  // PrepOut in 13 words
+  uint32_t h[8];
+  uint32_t ts_lo, ts_hi, hash_rel, hash_len, flags;
+};
+
 __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const PrepArgs a, const PrepCertArgs p) {
+#if MOCHI_PREP_LDS_STORE
+  __shared__ PrepOutLds lo[256];
+  __shared__ uint16_t ref[kPrepBlockGrants];
+  const uint32_t c0 = blockIdx.x * blockDim.x;
+  const uint32_t c_end = c0 + blockDim.x < p.n_certs ? c0 + blockDim.x : p.n_certs;
+  const uint32_t G0 = p.cert_grant_off[c0], G1 = p.cert_grant_off[c_end];
+  const bool staged = G1 - G0 <= kPrepBlockGrants;  // block-uniform
+  if (staged)
+    for (uint32_t i = threadIdx.x; i < G1 - G0; i += blockDim.x) ref[i] = 0xFFFFu;
+  __syncthreads();
+#else
+  const bool staged = false;
+  const uint32_t G0 = 0;
+  uint16_t* ref = nullptr;
+  PrepOutLds* lo = nullptr;
+#endif
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= p.n_certs) return;
-  const uint32_t g_lo = p.cert_grant_off[c], g_hi = p.cert_grant_off[c + 1];
-  uint64_t seen = 0;  // key slots < 64 whose first grant came already (others: a scan back)
-  uint32_t leaders = 0;
+  if (c < p.n_certs) {
+    const uint32_t g_lo = p.cert_grant_off[c], g_hi = p.cert_grant_off[c + 1];
+    uint64_t seen = 0;  // key slots < 64 whose first grant came already (others: a scan back)
+    uint32_t leaders = 0;
 #pragma unroll 1
-  for (uint32_t g = g_lo; g < g_hi; g++) {
-    const uint32_t s = p.grant_key[g];
-    bool first;
-    if (s < 64) {
-      first = !((seen >> s) & 1);
-      seen |= 1ull << s;
-    } else {
-      first = true;
+    for (uint32_t g = g_lo; g < g_hi; g++) {
+      const uint32_t s = p.grant_key[g];
+      bool first;
+      if (s < 64) {
+        first = !((seen >> s) & 1);
+        seen |= 1ull << s;
+      } else {
+        first = true;
 #pragma unroll 1
-      for (uint32_t q = g_lo; q < g; q++)
-        if (p.grant_key[q] == s) {
-          first = false;
-          break;
+        for (uint32_t q = g_lo; q < g; q++)
+          if (p.grant_key[q] == s) {
+            first = false;
+            break;
+          }
+      }
+      if (!first) continue;  // decided in its slot's first grant's pass
+      if (leaders++ == 2) break;  // a third slot: its grants are left to k_grant_prep_rare (rare stays 1)
+      // g leads its slot: prep it, then hand its results to every later grant of the
+      // slot with the same bytes; a grant that differs stays flagged
+      const bool via_lds = staged && leaders == 1;
+      PrepOut o;
+      const uint64_t og = a.goff[g];
+      const uint32_t lg = a.glen[g];
+      grant_prep_bytes(a.blob + og, lg, o);
+      if (via_lds) {
+        PrepOutLds& e = lo[threadIdx.x];
+#pragma unroll
+        for (int q = 0; q < 8; q++) e.h[q] = o.h[q];
+        e.ts_lo = (uint32_t)o.ts;
+        e.ts_hi = (uint32_t)((uint64_t)o.ts >> 32);
+        e.hash_rel = o.hash_rel;
+        e.hash_len = o.hash_len;
+        e.flags = o.flags;
+        ref[g - G0] = (uint16_t)threadIdx.x;
+      } else {
+        grant_prep_store(a, g, o);
+        p.rare[g] = 0;
+      }
+#pragma unroll 1
+      for (uint32_t h = g + 1; h < g_hi; h++) {
+        if (p.grant_key[h] != s) continue;
+        const uint64_t oh = a.goff[h];
+        const bool eq = (p.same && p.same[h] == g) ||
+                        (a.glen[h] == lg && (oh == og || bytes_equal(a.blob + oh, a.blob + og, lg)));
+        if (!eq) continue;
+        if (via_lds) {
+          ref[h - G0] = (uint16_t)threadIdx.x;
+        } else {
+          grant_prep_store(a, h, o);
+          p.rare[h] = 0;
         }
-    }
-    if (!first) continue;  // decided in its slot's first grant's pass
-    if (leaders++ == 2) {  // a third slot: its grants are left to k_grant_prep_rare (rare stays 1)
-      break;
-    }
-    // g leads its slot: prep it, then hand its results to every later grant of the
-    // slot with the same bytes; a grant that differs stays flagged
-    PrepOut o;
-    const uint64_t og = a.goff[g];
-    const uint32_t lg = a.glen[g];
-    grant_prep_bytes(a.blob + og, lg, o);
-    grant_prep_store(a, g, o);
-    p.rare[g] = 0;
-#pragma unroll 1
-    for (uint32_t h = g + 1; h < g_hi; h++) {
-      if (p.grant_key[h] != s) continue;
-      const uint64_t oh = a.goff[h];
-      const bool eq = (p.same && p.same[h] == g) ||
-                      (a.glen[h] == lg && (oh == og || bytes_equal(a.blob + oh, a.blob + og, lg)));
-      if (!eq) continue;
-      grant_prep_store(a, h, o);
-      p.rare[h] = 0;
+      }
     }
   }
+#if MOCHI_PREP_LDS_STORE
+  __syncthreads();
+  if (staged) {
+#pragma unroll 1
+    for (uint32_t i = threadIdx.x; i < G1 - G0; i += blockDim.x) {
+      const uint32_t r = ref[i];
+      if (r == 0xFFFFu) continue;  // a rare grant, or a second slot's (stored directly)
+      const PrepOutLds& e = lo[r];
+      PrepOut o;
+#pragma unroll
+      for (int q = 0; q < 8; q++) o.h[q] = e.h[q];
+      o.ts = (int64_t)(((uint64_t)e.ts_hi << 32) | e.ts_lo);
+      o.hash_rel = e.hash_rel;
+      o.hash_len = e.hash_len;
+      o.flags = (uint8_t)e.flags;
+      grant_prep_store(a, G0 + i, o);
+      p.rare[G0 + i] = 0;
+    }
+  }
+#endif
 }
 
 // The flagged grants, compacted per block: each block scans kRareSpan flags
