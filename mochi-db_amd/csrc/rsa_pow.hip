@@ -52,6 +52,9 @@
 #ifndef MOCHI_POW_DYN
 #define MOCHI_POW_DYN 1
 #endif
+#ifndef MOCHI_POW_NEXT_AHEAD
+#define MOCHI_POW_NEXT_AHEAD 1  // the next group's index fetched one group ahead (below)
+#endif
 namespace mochi {
 #if MOCHI_POW_STAMPS
 __device__ unsigned long long g_pow_stamps[4096][5];
@@ -108,13 +111,26 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
   uint32_t cur_key = 0xFFFFFFFFu;
 #if MOCHI_POW_DYN
   // groups from a device counter (zeroed by k_bucket_scan), double-buffered
-  // in LDS so one barrier per fetch suffices
+  // in LDS.  The next group's index is fetched at the start of this one and
+  // published at its end, so the atomic's round trip runs under this group's
+  // signature loads instead of stalling every wave at the group boundary.
   __shared__ uint32_t s_grp[2];
+  if (threadIdx.x == 0) s_grp[0] = atomicAdd(a.ctr, 1u);
+  __syncthreads();
   for (uint32_t it_g = 0;; it_g ^= 1) {
-    if (threadIdx.x == 0) s_grp[it_g] = atomicAdd(a.ctr, 1u);
-    __syncthreads();
     const uint32_t grp = __builtin_amdgcn_readfirstlane(s_grp[it_g]);
     if (grp >= n_groups) break;
+    uint32_t nxt = 0;
+    if (threadIdx.x == 0) nxt = atomicAdd(a.ctr, 1u);
+#if !MOCHI_POW_NEXT_AHEAD  // A/B: wait for the fetch here, as every wave did before
+    if (threadIdx.x == 0) s_grp[it_g ^ 1] = nxt;
+    __syncthreads();
+#endif
+    // publishes the next index: every path through the group body ends here
+    auto publish = [&]() {
+      if (MOCHI_POW_NEXT_AHEAD && threadIdx.x == 0) s_grp[it_g ^ 1] = nxt;
+      __syncthreads();
+    };
 #else
   const uint32_t g_begin = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
   const uint32_t g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
@@ -124,7 +140,12 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
     // buckets are 512-aligned and padded only at their tail: a group whose
     // first slot is empty is all padding (every thread reads the same slot)
     const uint32_t g_lead = __builtin_amdgcn_readfirstlane(a.perm[base]);
-    if (g_lead == 0xFFFFFFFFu) continue;
+    if (g_lead == 0xFFFFFFFFu) {
+#if MOCHI_POW_DYN
+      publish();
+#endif
+      continue;
+    }
     const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)a.signer[g_lead]);
     if (key != cur_key) {
       __syncthreads();  // the old image is no longer read
@@ -139,6 +160,9 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
     if (__ballot(active) == 0) {  // this wave's quarter of the group is padding: keep the barrier count
 #pragma unroll 1
       for (int i = 0; i < 33; i++) phase_barrier();
+#if MOCHI_POW_DYN
+      publish();
+#endif
       continue;
     }
     if (lag) phase_barrier();  // phase 0: the partner squares, this wave waits its turn
@@ -173,6 +197,9 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
       for (int q = 0; q < kL; q++) a.zout[(size_t)q * a.n_slots + slot] = x[q];
     }
     if (!lag) phase_barrier();  // phase 32: the partner folds its last squaring
+#if MOCHI_POW_DYN
+    publish();
+#endif
   }
 #if MOCHI_POW_STAMPS
   const uint64_t t_end = stamp();
