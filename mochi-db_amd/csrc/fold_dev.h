@@ -140,29 +140,54 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
 // block b takes a contiguous range of groups; fn(base, key) runs per non-empty
 // group after the signer's fold image is staged in `w` (restaged only when the
 // key changes along the range — block-uniform).
+// ctr (optional): groups are taken from this device counter (zeroed before the
+// launch) instead of a contiguous range -- a CU that starts late or clocks lower
+// does fewer; the next index is fetched one group ahead, so the atomic's round
+// trip runs under the current group
 template <typename F>
 __device__ __forceinline__ void for_groups(const uint32_t* __restrict__ perm, uint32_t n_slots,
                                            const uint16_t* __restrict__ signer, const FoldKey* __restrict__ fold,
-                                           v4i* w, F&& fn) {
+                                           v4i* w, F&& fn, uint32_t* ctr = nullptr) {
   const uint32_t n_groups = (n_slots + kBucketAlign - 1) / kBucketAlign;
-  const uint32_t g_begin = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
-  const uint32_t g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
+  __shared__ uint32_t s_grp[2];
+  const bool dyn = ctr != nullptr;  // kernel argument: uniform
+  uint32_t grp, g_end, it = 0;
+  if (dyn) {
+    if (threadIdx.x == 0) s_grp[0] = atomicAdd(ctr, 1u);
+    __syncthreads();
+    grp = __builtin_amdgcn_readfirstlane(s_grp[0]);
+    g_end = n_groups;
+  } else {
+    grp = (uint32_t)((uint64_t)blockIdx.x * n_groups / gridDim.x);
+    g_end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n_groups / gridDim.x);
+  }
   uint32_t cur_key = 0xFFFFFFFFu;
-  for (uint32_t grp = g_begin; grp < g_end; grp++) {
+  while (grp < g_end) {
+    uint32_t nxt = 0;
+    if (dyn && threadIdx.x == 0) nxt = atomicAdd(ctr, 1u);
     const uint32_t base = grp * kBucketAlign;
     // buckets are 512-aligned and padded only at their tail: a group whose
     // first slot is empty is all padding (every thread reads the same slot)
     const uint32_t g_lead = __builtin_amdgcn_readfirstlane(perm[base]);
-    if (g_lead == 0xFFFFFFFFu) continue;
-    const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)signer[g_lead]);
-    if (key != cur_key) {
-      __syncthreads();  // the old image is no longer read
-      const v4i* src = (const v4i*)fold[key].img;
-      for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
-      __syncthreads();
-      cur_key = key;
+    if (g_lead != 0xFFFFFFFFu) {
+      const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)signer[g_lead]);
+      if (key != cur_key) {
+        __syncthreads();  // the old image is no longer read
+        const v4i* src = (const v4i*)fold[key].img;
+        for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
+        __syncthreads();
+        cur_key = key;
+      }
+      fn(base, key, g_lead);
     }
-    fn(base, key, g_lead);
+    if (dyn) {
+      it ^= 1;
+      if (threadIdx.x == 0) s_grp[it] = nxt;
+      __syncthreads();
+      grp = __builtin_amdgcn_readfirstlane(s_grp[it]);
+    } else {
+      grp++;
+    }
   }
 }
 

@@ -28,6 +28,11 @@
 #include "fold_dev.h"
 #include "rsa_common.h"
 
+// groups from a device counter (fold_dev.h for_groups), as k_rsa_pow's
+#ifndef MOCHI_FINAL_DYN
+#define MOCHI_FINAL_DYN 1
+#endif
+
 namespace mochi {
 namespace {
 
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
                                                        const FoldKey* __restrict__ fold,
                                                        const uint32_t* __restrict__ zin,
                                                        const uint32_t* __restrict__ digest, uint32_t n_grants,
-                                                       uint8_t* __restrict__ flags) {
+                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ ctr) {
   __shared__ v4i w[kFoldImgBytes / 16];
   for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
     // (the next half's operands loaded while this half computes -- into AGPRs,
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
       final_load(base + h + threadIdx.x, g_lead, perm, n_slots, sig, zin, o);
       final_slot(o, key, g_lead, keys, fold, digest, n_grants, flags, w);
     }
-  });
+  }, MOCHI_FINAL_DYN ? ctr : nullptr);
 }
 
 }  // namespace
@@ -162,7 +167,7 @@ void launch_rsa_final(const LaunchArgs& a, hipStream_t st) {
   const uint32_t blocks = fold_grid(a.n_slots);
   if (!blocks) return;
   hipLaunchKernelGGL(k_rsa_final, dim3(blocks), dim3(256), 0, st, a.perm, a.n_slots, a.sig, a.signer, a.keys, a.fold,
-                     a.xbuf, a.digest, a.n_grants, a.flags);
+                     a.xbuf, a.digest, a.n_grants, a.flags, a.total + kTotFinalGroup);
 }
 
 }  // namespace mochi
