@@ -28,7 +28,8 @@ namespace mochi {
 // k_grant_prep: parse + SHA-256, certificate order (lane = grant).
 // ---------------------------------------------------------------------------
 #ifndef MOCHI_PREP_WAVES
-#define MOCHI_PREP_WAVES 0  // A/B builds: amdgpu_waves_per_eu for k_grant_prep (0 = the compiler's choice)
+#define MOCHI_PREP_WAVES 4  // amdgpu_waves_per_eu for the prep kernels: k_grant_prep_cert fits 126 VGPRs unspilled
+                            // (133 uncapped: 3 waves); prep outside the serial stages 0.86 -> 0.83 ms
 #endif
 #if MOCHI_PREP_WAVES
 #define MOCHI_PREP_ATTR __attribute__((amdgpu_waves_per_eu(MOCHI_PREP_WAVES)))
