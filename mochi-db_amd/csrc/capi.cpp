@@ -925,7 +925,7 @@ int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_
   a->cnt_ce = cnt + 6 * m1;
   a->ce = cnt + (size_t)mochi::kW2MsgArrays * m1;
   a->ce_cap = mochi::kW2MaxCertEntries * (uint32_t)m1;
-  a->inl = (uint32_t*)(((uintptr_t)(a->ce + 11 * (size_t)a->ce_cap) + 15) & ~(uintptr_t)15);
+  a->inl = (uint32_t*)(((uintptr_t)(a->ce + mochi::kW2CeArrays * (size_t)a->ce_cap) + 15) & ~(uintptr_t)15);
   a->inl_ops = a->inl + 4 * (size_t)mochi::kW2InlEntries * m1;
   a->cnt4 = a->inl_ops + 2 * (size_t)mochi::kW2InlOps * m1;  // 16-byte aligned: the two above are multiples of 4 words
   a->off4 = a->cnt4 + 4 * m1;

@@ -26,7 +26,7 @@ struct W2Args {
   uint32_t* cnt_m;  // [M+1] MultiGrants
   // level-by-level decode: cnt_ce, ce_base, st_bits, wc_off, wc_len, tx_off,
   // tx_len ([M+1] each, contiguous from cnt_ce) and the certificate-entry list
-  // (11 arrays of ce_cap words)
+  // (kW2CeArrays arrays of ce_cap words)
   uint32_t* cnt_ce;
   uint32_t* ce;
   uint32_t ce_cap;
@@ -57,10 +57,11 @@ struct W2Args {
 };
 // Device words of one decode's per-batch scratch: 13 arrays of M+1 (counts,
 // CSR offsets, level-1 state) + the certificate-entry list (at most
-// kW2MaxCertEntries per message on the fast path, 11 words each) + level 1's
-// entry records + the packed per-message counts and their scan.
+// kW2MaxCertEntries per message on the fast path, kW2CeArrays words each) +
+// level 1's entry records + the packed per-message counts and their scan.
 constexpr uint32_t kW2MaxCertEntries = 32;
 constexpr int kW2MsgArrays = 13;
+constexpr int kW2CeArrays = 12;
 // Level 1 records the key / value slices of a message's first kW2InlEntries
 // certificate entries, so the compact entry list is copied, not re-parsed.
 constexpr uint32_t kW2InlEntries = 4;
@@ -68,7 +69,7 @@ constexpr uint32_t kW2InlEntries = 4;
 // 2's key-slot lookup compares keys instead of re-walking the transaction.
 constexpr uint32_t kW2InlOps = 4;
 inline size_t w2_scratch_words(uint32_t M) {
-  return (size_t)kW2MsgArrays * ((size_t)M + 1) + 11 * (size_t)kW2MaxCertEntries * ((size_t)M + 1) +
+  return (size_t)kW2MsgArrays * ((size_t)M + 1) + kW2CeArrays * (size_t)kW2MaxCertEntries * ((size_t)M + 1) +
          4 * (size_t)kW2InlEntries * ((size_t)M + 1) + 2 * (size_t)kW2InlOps * ((size_t)M + 1) + 8 * ((size_t)M + 1) +
          4;  // + 4: 16-byte alignment
 }

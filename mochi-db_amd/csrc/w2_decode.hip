@@ -616,6 +616,8 @@ struct MGScan {
   Entry g, sg;               // last grants / grantSignatures entry
   uint32_t sid_off, sid_len;  // MultiGrant.serverId (last)
   bool first_nc;             // the first grants entry holds one value, parsed and not canonical
+  bool same;                 // the grant's bytes equal the reference grant's (prep reuses its results)
+  bool sig_key;              // mg_match: the signature entry's key is the grant's
 };
 
 __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan& m, const RefGrant ref = RefGrant{}) {
@@ -624,7 +626,7 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
   int rc;
   m.nge = m.nse = 0;
   m.sid_off = m.sid_len = 0;
-  m.first_nc = false;
+  m.first_nc = m.sig_key = false;
 #pragma unroll 1
   while ((rc = next_fld(r, pos, end, f)) > 0) {
     if (f.wt != 2) continue;
@@ -643,7 +645,171 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
       if (!valid_leaf_read(r, f.off, f.len, 0, m.sg)) return false;
     }
   }
+  m.same = m.nge == 1 && m.g.assumed;
   return rc == 0;
+}
+
+// ---- the reference encoder's MultiGrant, matched from a few wide loads ------
+// encode_multigrant / protobuf-java (MochiProtocol.proto:117-124 + field 5):
+// one grant, fields in number order, each map entry its key then its value,
+//   0x0A L1 { 0x0A kl key 0x12 gl Grant } 0x22 sl serverId
+//   0x2A L5 { 0x0A kl key 0x12 0x80 0x02 signature[256] }
+// the signature entry under the grant's key, key and serverId ASCII (kl, sl <= 60),
+// L1 and gl one or two varint bytes, and the Grant itself in its common
+// canonical shape 0x0A L objectId 0x10 ts 0x22 H transactionHash (<= 192 bytes,
+// ASCII strings).  Every position follows from the first 16 bytes (the
+// signature entry's from the value's end), so the loads after the first are
+// independent of each other -- three load latencies (header, windows, the
+// grant's timestamp) where the walk (next_fld / ByteReader::at) paid one per
+// field, length and word.  Any difference returns false and valid_mg_scan
+// decides; what this accepts, valid_mg_scan accepts with the same MGScan (one
+// grants and one grantSignatures entry of one key and one value each, the grant
+// parsed and canonical -- parse_grant_t's CANON rules).
+#ifndef MOCHI_W2_MATCH
+#define MOCHI_W2_MATCH 1  // A/B: 0 = every MultiGrant through valid_mg_scan
+#endif
+
+__device__ __forceinline__ uint32_t wbyte(const uint32_t* w, uint32_t k) {  // k compile-time after unrolling
+  return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+}
+
+// bytes [a, b) of a window, as a mask of word t
+__device__ __forceinline__ uint32_t span_mask(int t, int a, int b) {
+  const int lo = a - 4 * t, hi = b - 4 * t;
+  const uint32_t m_hi = hi >= 4 ? ~0u : hi <= 0 ? 0u : (1u << (8 * hi)) - 1u;
+  const uint32_t m_lo = lo <= 0 ? 0u : lo >= 4 ? ~0u : (1u << (8 * lo)) - 1u;
+  return m_hi & ~m_lo;
+}
+
+// The common Grant shape, canonical and valid (ASCII strings), from its own
+// windows: `hib` = bytes with the high bit set over the whole grant, w0 = its
+// first 16 bytes, read from the timestamp's tag on with one more window.
+__device__ __forceinline__ bool grant_match(const uint8_t* base, uint32_t mlen, uint32_t g0, uint32_t gl,
+                                            const uint32_t (&w0)[16], uint32_t hib) {
+  const uint32_t L = wbyte(w0, 1);
+  if (wbyte(w0, 0) != 0x0Au || L == 0 || L >= 0x80u || L + 6 > gl) return false;
+  uint32_t tb[4];
+  window16(base, mlen, g0 + 2 + L, tb);
+  if (wbyte(tb, 0) != 0x10u) return false;
+  // timestamp: 1..9 varint bytes, minimal (nonzero last byte; a one-byte 0 is the default, never written)
+  uint32_t k = 0, last = 0;
+  bool end = false;
+#pragma unroll
+  for (uint32_t i = 1; i <= 9; i++) {
+    const uint32_t c = wbyte(tb, i);
+    if (!end) {
+      k = i;
+      last = c;
+      end = c < 0x80u;
+    }
+  }
+  if (!end || last == 0) return false;
+  uint32_t c1 = 0, c2 = 0, tag = 0;  // the bytes after the timestamp (k + 1 <= 10)
+#pragma unroll
+  for (uint32_t i = 2; i <= 10; i++) {
+    if (i == k + 1) {
+      tag = wbyte(tb, i);
+      c1 = wbyte(tb, i + 1);
+      c2 = wbyte(tb, i + 2);
+    }
+  }
+  if (tag != 0x22u) return false;
+  uint32_t hl, nh;
+  if (c1 < 0x80u) {
+    hl = c1;
+    nh = 1;
+  } else if (c2 < 0x80u && c2 != 0) {
+    hl = (c1 & 0x7Fu) | (c2 << 7);
+    nh = 2;
+  } else {
+    return false;
+  }
+  const uint32_t hp = 2 + L + 1 + k + 1 + nh;
+  return hl != 0 && hp + hl == gl && hib == (k - 1) + (nh - 1);
+}
+
+// kw / sw (out): the windows at the grants entry (0x0A kl key) and at the
+// serverId (0x22 sl serverId), for the signer and key-slot lookups
+__device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, const RefGrant ref, MGScan& m, uint32_t (&kw)[16],
+                         uint32_t (&sw)[16]) {
+  const uint8_t* base = r.base;
+  const uint32_t mlen = r.len;
+  if (vl < 272) return false;
+  uint32_t h[4];
+  window16(base, mlen, vo, h);
+  const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
+  uint32_t n1, L1, et, kl;
+  if (c1 < 0x80u) {
+    n1 = 1;
+    L1 = c1;
+    et = c2;
+    kl = wbyte(h, 3);
+  } else if (c2 < 0x80u) {
+    n1 = 2;
+    L1 = (c1 & 0x7Fu) | (c2 << 7);
+    et = wbyte(h, 3);
+    kl = wbyte(h, 4);
+  } else {
+    return false;
+  }
+  if (wbyte(h, 0) != 0x0Au || et != 0x0Au || kl > 60) return false;
+  const uint32_t e1 = vo + 1 + n1, s_tag = e1 + L1, end = vo + vl;
+  const uint32_t p5 = end - 264 - kl;  // the signature entry's tag (its key: kl bytes, as the grant's)
+  if (L1 < kl + 3 + 1 + 8 || s_tag + 2 > p5 || p5 - s_tag - 2 > 60) return false;
+  const uint32_t sl = p5 - s_tag - 2;
+  const uint32_t rest = L1 - 3 - kl;  // gl + its varint
+  if (rest == 129) return false;     // gl = 127 in two bytes: not minimal
+  const uint32_t n2 = rest <= 128 ? 1u : 2u, gl = rest - n2;
+  const uint32_t gpos = e1 + 2 + kl, g0 = gpos + 1 + n2;
+  if (gl > 192) return false;
+  // ---- independent loads: framing words, key / serverId windows, the grant ----
+  const uint32_t gh = ld4(base, gpos), t5 = ld4(base, p5), sh = ld4(base, end - 259);
+  uint32_t(&k1)[16] = kw;
+  uint32_t k4[16];
+  window64(base, mlen, e1, k1);      // 0x0A kl key
+  window64(base, mlen, p5 + 3, k4);  // 0x0A kl key (the signature entry's)
+  window64(base, mlen, s_tag, sw);   // 0x22 sl serverId
+  const uint32_t L5 = 261 + kl;
+  bool ok = (gh & 0xFFu) == 0x12u &&
+            (n2 == 1 ? ((gh >> 8) & 0xFFu) == gl : ((gh >> 8) & 0xFFFFu) == (((gl & 0x7Fu) | 0x80u) | ((gl >> 7) << 8))) &&
+            t5 == (0x2Au | (((L5 & 0x7Fu) | 0x80u) << 8) | ((L5 >> 7) << 16) | (0x0Au << 24)) &&
+            (sh & 0xFFFFFFu) == 0x028012u && (sw[0] & 0xFFFFu) == (0x22u | (sl << 8));
+  uint32_t kdiff = 0, hi = 0;
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    kdiff |= (k1[t] ^ k4[t]) & span_mask(t, 0, 2 + (int)kl);
+    hi |= k1[t] & span_mask(t, 2, 2 + (int)kl);
+    hi |= sw[t] & span_mask(t, 2, 2 + (int)sl);
+  }
+  ok = ok && kdiff == 0 && (hi & 0x80808080u) == 0;
+  // ---- the grant: its high-bit count, its first window, and the compare with the reference grant ----
+  const bool cmp = ref.off != ~0u && ref.len == gl;
+  uint32_t w0[16], hib = 0, gdiff = 0;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    if (64u * c < gl) {
+      uint32_t w[16], v[16];
+      window64(base, mlen, g0 + 64 * c, w);
+      if (cmp) window64(base, mlen, ref.off + 64 * c, v);
+#pragma unroll
+      for (int t = 0; t < 16; t++) {
+        const uint32_t mk = span_mask(t, 0, (int)gl - 64 * c);
+        hib += __builtin_popcount(w[t] & mk & 0x80808080u);
+        if (cmp) gdiff |= (w[t] ^ v[t]) & mk;
+        if (c == 0) w0[t] = w[t];
+      }
+    }
+  }
+  if (!ok || !grant_match(base, mlen, g0, gl, w0, hib)) return false;
+  m.nge = m.nse = 1;
+  m.g = Entry{e1 + 2, kl, g0, gl, 1, true, false};
+  m.sg = Entry{p5 + 5, kl, end - 256, 256, 1, false, false};
+  m.sid_off = s_tag + 2;
+  m.sid_len = sl;
+  m.first_nc = false;
+  m.same = cmp && gdiff == 0;
+  m.sig_key = true;
+  return true;
 }
 
 // signer = index of the key whose server id is the MultiGrant's serverId.
@@ -656,10 +822,14 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
 // it with LDS words (the same address in every lane: a broadcast) instead of
 // a byte-compare loop of dependent global loads per candidate.
 constexpr uint32_t kIdTab = 64, kIdTabWords = 1024, kIdFast = 16;  // ids, LDS words, words compared from registers
+constexpr uint32_t kSidWords = 15;  // serverId words hashed / compared from mg_match's window (<= 60 bytes)
 struct IdTab {
   uint32_t len[kIdTab], tail[kIdTab], pos[kIdTab];  // pos: first LDS word, ~0 = not staged
+  uint32_t hash[kIdTab];                            // sid_mix over the id's first kSidWords words
   uint32_t w[kIdTabWords];
 };
+
+__device__ __forceinline__ uint32_t sid_mix(uint32_t h, uint32_t w) { return (h ^ w) * 0x9E3779B1u; }
 
 __device__ __forceinline__ void stage_ids(IdTab& tab, const uint8_t* __restrict__ ids,
                                           const uint32_t* __restrict__ id_off, uint32_t n_ids) {
@@ -676,6 +846,13 @@ __device__ __forceinline__ void stage_ids(IdTab& tab, const uint8_t* __restrict_
   for (uint32_t k = threadIdx.x; k < n_ids && k < kIdTab; k += blockDim.x) {
     const uint32_t o = id_off[k], l = tab.len[k];
     tab.tail[k] = l >= 4 ? ld4(ids, o + l - 4) : 0u;
+    uint32_t h = 0;
+    for (uint32_t t = 0; t < kSidWords; t++) {
+      uint32_t v = 0;
+      for (uint32_t j = 0; j < 4 && 4 * t + j < l; j++) v |= (uint32_t)ids[o + 4 * t + j] << (8 * j);
+      h = sid_mix(h, v);
+    }
+    tab.hash[k] = h;
     if (tab.pos[k] != ~0u)
       for (uint32_t t = 0; 4 * t < l; t++) {
         uint32_t v = 0;
@@ -779,21 +956,130 @@ __device__ __forceinline__ uint8_t find_key_slot_rec(ByteReader& r, const W2Msg&
   return 0xFF;
 }
 
+// find_signer from mg_match's serverId window (0x22 sl serverId, sl <= 60): the
+// id of this length and hash (IdTab::hash) is compared word by word with the
+// LDS copy -- no load of the message.  Several candidates (equal ids, a hash
+// collision), an unstaged id or a table past kIdTab: find_signer.
+__device__ __forceinline__ uint16_t signer_from_window(ByteReader& r, uint32_t so, uint32_t sl, const uint32_t (&sw)[16],
+                                                       const uint8_t* __restrict__ ids,
+                                                       const uint32_t* __restrict__ id_off, uint32_t n_ids,
+                                                       const IdTab& tab) {
+  uint32_t w[kSidWords], h = 0;
+#pragma unroll
+  for (int t = 0; t < (int)kSidWords; t++) {
+    w[t] = __builtin_amdgcn_alignbit(sw[t + 1], sw[t], 16) & span_mask(t, 0, (int)sl);
+    h = sid_mix(h, w[t]);
+  }
+  if (n_ids <= kIdTab) {
+    uint32_t cand = ~0u, nc = 0;
+#pragma unroll 1
+    for (uint32_t k = 0; k < n_ids; k++)
+      if (tab.len[k] == sl && tab.hash[k] == h && nc++ == 0) cand = k;
+    if (nc == 0) return 0xFFFF;
+    if (nc == 1 && tab.pos[cand] != ~0u) {
+      const uint32_t* tw = tab.w + tab.pos[cand];
+      uint32_t diff = 0;
+#pragma unroll
+      for (int t = 0; t < (int)kSidWords; t++)
+        if (4u * t < sl) diff |= w[t] ^ tw[t];  // the LDS copy's last word is zero-padded, as w's
+      return diff == 0 ? (uint16_t)cand : (uint16_t)0xFFFF;
+    }
+  }
+  return find_signer(r, so, sl, ids, id_off, n_ids, &tab);
+}
+
+// find_key_slot_rec from mg_match's key window (0x0A kl key): each recorded
+// operation key of this length is loaded as one window from two bytes before
+// it (its tag and length) and compared with the key's bytes in registers
+__device__ __forceinline__ uint8_t slot_from_window(ByteReader& r, const W2Msg& s, uint32_t m, uint32_t ko, uint32_t kl,
+                                                    const uint32_t (&kw)[16]) {
+  const uint32_t nops = s.cnt_o[m];
+  if (nops > kW2InlOps) return find_key_slot(r, s.tx_off[m], s.tx_len[m], ko, kl);
+  const uint2* q = (const uint2*)(s.inl_ops + (size_t)2 * kW2InlOps * m);
+  uint8_t slot = 0xFF;
+#pragma unroll
+  for (uint32_t j = 0; j < kW2InlOps; j++) {
+    if (j < nops) {
+      const uint2 o = q[j];
+      bool eq = o.y == kl;
+      if (eq && kl != 0) {  // an operand1 is preceded by its tag and length: o.x >= 2
+        uint32_t ow[16], diff = 0;
+        window64(r.base, r.len, o.x - 2, ow);
+#pragma unroll
+        for (int t = 0; t < 16; t++) diff |= (ow[t] ^ kw[t]) & span_mask(t, 2, 2 + (int)kl);
+        eq = diff == 0;
+      }
+      if (eq && slot == 0xFF) slot = (uint8_t)j;
+    }
+  }
+  return slot;
+}
+
+// The first grant of a MultiGrant value, as first_grant finds it, from one
+// window and one word (lengths of one or two varint bytes, a key < 128 bytes:
+// otherwise none -- the match is a hint, and only equal bytes use it).
+__device__ __forceinline__ RefGrant ref_grant_win(ByteReader& r, uint32_t off, uint32_t len) {
+  RefGrant g;
+  if (len < 8) return g;
+  uint32_t h[4];
+  window16(r.base, r.len, off, h);
+  const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
+  uint32_t n1, L1, et, kl;
+  if (c1 < 0x80u) {
+    n1 = 1;
+    L1 = c1;
+    et = c2;
+    kl = wbyte(h, 3);
+  } else if (c2 < 0x80u) {
+    n1 = 2;
+    L1 = (c1 & 0x7Fu) | (c2 << 7);
+    et = wbyte(h, 3);
+    kl = wbyte(h, 4);
+  } else {
+    return g;
+  }
+  const uint32_t e1 = off + 1 + n1;
+  if (wbyte(h, 0) != 0x0Au || et != 0x0Au || kl >= 0x80u || e1 + L1 > off + len || L1 < kl + 3 + 1 + 3) return g;
+  const uint32_t rest = L1 - 3 - kl;
+  if (rest == 129) return g;
+  const uint32_t n2 = rest <= 128 ? 1u : 2u, gl = rest - n2, gpos = e1 + 2 + kl;
+  const uint32_t gh = ld4(r.base, gpos);  // gpos + 4 <= the grant's end (gl >= 3)
+  const bool ok = (gh & 0xFFu) == 0x12u &&
+                  (n2 == 1 ? ((gh >> 8) & 0xFFu) == gl : ((gh >> 8) & 0xFFFFu) == (((gl & 0x7Fu) | 0x80u) | ((gl >> 7) << 8)));
+  if (ok) {
+    g.off = gpos + 1 + n2;
+    g.len = gl;
+  }
+  return g;
+}
+
 // Certificate entries (compact, in wire order per message): message index,
-// key and value slices (message-relative), the index of the entry holding the
-// key's final value (~0 unless this entry is the key's first), and the number
-// of distinct grants of a final-value entry.
+// key and value slices (message-relative), the key's last four bytes (all of
+// it, zero-padded, when shorter: k_w2_mg's sibling filter), the index of the
+// entry holding the key's final value (~0 unless this entry is the key's
+// first), and the number of distinct grants of a final-value entry.
 // A decoded MultiGrant with one distinct grant (the common shape) also leaves
 // its emit record here -- grant value slice, signature offset (message-
 // relative, ~0 = none), signer << 8 | key slot -- written by k_w2_mg while the
 // bytes are hot, so k_w2_emit_mg need not walk it again.
 struct CE {
   uint32_t *msg, *koff, *klen, *voff, *vlen, *last, *ng;
-  uint32_t *r_goff, *r_glen, *r_sig, *r_sk;
+  uint32_t *r_goff, *r_glen, *r_sig, *r_sk, *ktail;
 };
+static_assert(sizeof(CE) == kW2CeArrays * sizeof(uint32_t*), "kW2CeArrays (w2.h) counts the CE arrays");
 __host__ __device__ inline CE ce_view(uint32_t* p, uint32_t cap) {
   const size_t c = cap;
-  return CE{p, p + c, p + 2 * c, p + 3 * c, p + 4 * c, p + 5 * c, p + 6 * c, p + 7 * c, p + 8 * c, p + 9 * c, p + 10 * c};
+  return CE{p,         p + c,     p + 2 * c, p + 3 * c, p + 4 * c,  p + 5 * c,
+            p + 6 * c, p + 7 * c, p + 8 * c, p + 9 * c, p + 10 * c, p + 11 * c};
+}
+
+// the last four bytes of key [ko, ko + kl) of the message, little-endian (the
+// whole key, zero-padded, when it is shorter)
+__device__ __forceinline__ uint32_t key_tail(ByteReader& r, uint32_t ko, uint32_t kl) {
+  if (kl >= 4) return ld4(r.base, ko + kl - 4);
+  uint32_t v = 0;
+  for (uint32_t j = 0; j < kl; j++) v |= r.at(ko + j) << (8 * j);
+  return v;
 }
 
 // The distinct grants of one decoded MultiGrant value [mo, mo+ml), in map
@@ -943,9 +1229,11 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
   const uint32_t nce = s.cnt_ce[m];
   if (nce == 0) return;
   uint32_t e = s.ce_base[m];
+  ByteReader r;
+  r.init(wire + moff[m], mlen[m]);
   if (nce <= kW2InlEntries) {  // recorded by level 1: copy
     const uint4* q = (const uint4*)(s.inl + (size_t)4 * kW2InlEntries * m);
-#pragma unroll 1
+#pragma unroll 4
     for (uint32_t j = 0; j < nce; j++, e++) {
       const uint4 v = q[j];
       ce.msg[e] = m;
@@ -953,11 +1241,10 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
       ce.klen[e] = v.y;
       ce.voff[e] = v.z;
       ce.vlen[e] = v.w;
+      ce.ktail[e] = key_tail(r, v.x, v.y);
     }
     return;
   }
-  ByteReader r;
-  r.init(wire + moff[m], mlen[m]);
   uint32_t pos = s.wc_off[m];
   const uint32_t end = pos + s.wc_len[m];
   Fld f;
@@ -971,6 +1258,7 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
     ce.klen[e] = x.klen;
     ce.voff[e] = x.voff;
     ce.vlen[e] = x.vlen;
+    ce.ktail[e] = key_tail(r, x.koff, x.klen);
     e++;
   }
 }
@@ -1060,22 +1348,27 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
     const uint32_t m = ce.msg[e];
     ByteReader r;
     r.init(wire + moff[m], mlen[m]);
-    const uint32_t b0 = s.ce_base[m], b1 = s.ce_base[m + 1], ko = ce.koff[e], kl = ce.klen[e];
+    const uint32_t b0 = s.ce_base[m], b1 = s.ce_base[m + 1], ko = ce.koff[e], kl = ce.klen[e], kt = ce.ktail[e];
     bool first = true;
     uint32_t last = e;
-#pragma unroll 1
-    for (uint32_t j = b0; j < b1; j++)
-      if (j != e && key_eq(r, ce.koff[j], ce.klen[j], ko, kl)) {
-        if (j < e) first = false;
-        else last = j;
-      }
+    // siblings with this key: length and last four bytes from the entry list (a
+    // key of at most four bytes is all in them), the bytes compared only then
+#pragma unroll 4
+    for (uint32_t j = b0; j < b1; j++) {
+      if (j == e || ce.klen[j] != kl || ce.ktail[j] != kt) continue;
+      if (kl > 4 && !key_eq(r, ce.koff[j], kl, ko, kl)) continue;
+      if (j < e) first = false;
+      else last = j;
+    }
     const uint32_t vo = ce.voff[e], vl = ce.vlen[e];
     uint32_t bits = 0, ng = 0;
     MGScan sc;
     // the R MultiGrants of an honest certificate carry the same grant bytes:
     // a grant equal to the first MultiGrant's first grant is parsed by that
     // entry's lane only
-    const RefGrant ref = e != b0 ? first_grant(r, ce.voff[b0], ce.vlen[b0]) : RefGrant{};
+    const RefGrant ref = e == b0                ? RefGrant{}
+                         : MOCHI_W2_MATCH ? ref_grant_win(r, ce.voff[b0], ce.vlen[b0])
+                                          : first_grant(r, ce.voff[b0], ce.vlen[b0]);
     // the emit record, read by k_w2_emit_mg when ng == 1
     auto rec = [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
       ce.r_goff[e] = go;
@@ -1084,7 +1377,9 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
       ce.r_sk[e] = (uint32_t)sg << 8 | key;
     };
     stp.mark(1);
-    const bool valid = valid_mg_scan(r, vo, vl, sc, ref);
+    uint32_t kw[16], sw[16];
+    const bool fast = MOCHI_W2_MATCH && mg_match(r, vo, vl, ref, sc, kw, sw);
+    const bool valid = fast || valid_mg_scan(r, vo, vl, sc, ref);
     stp.mark(2);
     if (valid && e == b0 && sc.first_nc) bits |= kStFirstNC;  // the reference grant of this message's other lanes
     if (!valid) {
@@ -1101,13 +1396,18 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
           bits |= kStFb;
         } else {
           ng = 1;
-          const bool have = sc.nse == 1 && key_eq(r, sc.sg.koff, sc.sg.klen, sc.g.koff, sc.g.klen);
-          const uint16_t signer = find_signer(r, sc.sid_off, sc.sid_len, ids, id_off, n_ids, &tab);
+          const bool have = sc.nse == 1 && (sc.sig_key || key_eq(r, sc.sg.koff, sc.sg.klen, sc.g.koff, sc.g.klen));
+          const uint16_t signer = fast ? signer_from_window(r, sc.sid_off, sc.sid_len, sw, ids, id_off, n_ids, tab)
+                                       : find_signer(r, sc.sid_off, sc.sid_len, ids, id_off, n_ids, &tab);
           stp.mark(4);
-          const uint8_t slot = find_key_slot_rec(r, s, m, sc.g.koff, sc.g.klen);
+          const uint8_t slot = fast ? slot_from_window(r, s, m, sc.g.koff, sc.g.klen, kw)
+                                    : find_key_slot_rec(r, s, m, sc.g.koff, sc.g.klen);
           stp.mark(5);
           rec(sc.g.voff, sc.g.vlen, signer, have && sc.sg.vlen == MOCHI_RSA_BYTES ? sc.sg.voff : ~0u, slot);
-          if (sc.g.assumed) ce.r_sk[e] |= 1u << 31;  // its bytes are the message's first grant's (k_w2_emit_mg)
+          // bit 31: its bytes are the message's first grant's (k_w2_emit_mg); bit 30: the
+          // emitted grant IS the value's first grant (one grants entry, one value), so on
+          // the first entry it is the grant the other entries were compared with
+          ce.r_sk[e] |= (sc.same ? 1u << 31 : 0u) | 1u << 30;
         }
       } else if (sc.nge > kMaxGrantsPerMG || sc.nse > kMaxSigEntries ||
                  !mg_decode_first(r, vo, vl, s.tx_off[m], s.tx_len[m], ids, id_off, n_ids, ng, rec)) {
@@ -1191,7 +1491,7 @@ __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ 
       // the same bytes as the message's first grant -- the first one emitted
       // (base.x) when the first entry holds its key's final value, one grant
       const uint32_t b0 = s.ce_base[m];
-      const bool same = (sk >> 31) && L != b0 && ce.last[b0] == b0 && ce.ng[b0] == 1;
+      const bool same = (sk >> 31) && L != b0 && ce.last[b0] == b0 && ce.ng[b0] == 1 && ((ce.r_sk[b0] >> 30) & 1u);
       emit_grant(out, g, mo, ce.r_goff[L], ce.r_glen[L], (uint16_t)(sk >> 8), ce.r_sig[L], (uint8_t)sk,
                  same ? base.x : ~0u);
       continue;

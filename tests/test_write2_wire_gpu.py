@@ -571,3 +571,108 @@ def test_ten_byte_varint_garbage_is_not_canonical(pool4):
     assert st[0] == mh.MSG_OK and st[1] == mh.MSG_FALLBACK, st
     np.testing.assert_array_equal(g.cert_reason, o.cert_reason)
     ver.close()
+
+
+def _bad_key_byte(m, oid):
+    """m with the last byte of its first grants entry's key made 0xFF (invalid UTF-8)."""
+    kb = oid.encode()
+    pat = b"\x0a" + bytes([len(kb)]) + kb + b"\x12"
+    assert pat in m
+    return m.replace(pat, pat[:-2] + b"\xff\x12", 1)
+
+
+def _matcher_forms(s, c, ids):
+    """Certificate c re-encoded at and around the edges of k_w2_mg's layout matcher
+    (mg_match: the reference encoder's one-grant MultiGrant, ASCII key and serverId
+    <= 60 bytes, signature entry under the grant's key, Grant in its common canonical
+    shape <= 192 bytes).  Each form is legal protobuf; the matcher either decodes it
+    exactly as the walk does or leaves it to the walk."""
+    b = s.batch
+    g0, g1 = int(b.cert_grant_off[c]), int(b.cert_grant_off[c + 1])
+    items = []
+    for g in range(g0, g1):
+        gb = b.grant_bytes[int(b.grant_off[g]):int(b.grant_off[g]) + int(b.grant_len[g])].tobytes()
+        items.append((int(b.signer[g]), W.grant_object_id(gb), gb, b.sig[g].tobytes()))
+    r0, oid, gb, _ = items[0]
+    p = O.grant_parse(gb)
+    ts, th = int(p["timestamp"]), p["transaction_hash"].decode()
+    th_alt = th[:-1] + ("0" if th[-1] != "0" else "1")
+
+    def msg(grant_of=lambda r, g: g, key_of=lambda r, o: o, sig_key_of=None, sid_of=lambda r: ids[r],
+            sig_of=lambda r, sg: sg, extra_of=None, op_key=None):
+        ent = []
+        for r, o, g, sg in items:
+            k = key_of(r, o)
+            sk = sig_key_of(r, k) if sig_key_of else k
+            gl = grant_of(r, g)
+            grants = gl if isinstance(gl, list) else [(k, gl)]
+            mg = W.encode_multigrant(grants, sid_of(r), "", "", [(sk, sig_of(r, sg))])
+            ent.append((ids[r], mg + (extra_of(r) if extra_of else b"")))
+        return W.encode_write2(ent, [W.encode_operation(2, op_key if op_key is not None else key_of(r0, oid))])
+
+    return {
+        "plain": msg(),
+        "sig_under_other_key": msg(sig_key_of=lambda r, k: k + "x"),
+        "key_60": msg(key_of=lambda r, o: (o + "-" + "k" * 60)[:60]),
+        "key_61": msg(key_of=lambda r, o: (o + "-" + "k" * 61)[:61]),
+        "key_non_ascii": msg(key_of=lambda r, o: o + "é"),
+        "sid_non_ascii": msg(sid_of=lambda r: ids[r] + "é"),
+        "sid_61": msg(sid_of=lambda r: (ids[r] + "-" + "s" * 61)[:61]),
+        "sig_255": msg(sig_of=lambda r, sg: sg[:255]),
+        "trailing_unknown": msg(extra_of=lambda r: b"\x48\x07"),
+        "short_grant": msg(grant_of=lambda r, g: W.encode_grant(oid, ts, "ab")),
+        "grant_hash_127": msg(grant_of=lambda r, g: W.encode_grant(oid, ts, "c" * 127)),
+        "grant_hash_128": msg(grant_of=lambda r, g: W.encode_grant(oid, ts, "c" * 128)),
+        "grant_ts_1": msg(grant_of=lambda r, g: W.encode_grant(oid, 1, th)),
+        "grant_ts_9_bytes": msg(grant_of=lambda r, g: W.encode_grant(oid, 1 << 62, th)),
+        "grant_ts_negative": msg(grant_of=lambda r, g: W.encode_grant(oid, -7, th)),
+        "grant_configstamp": msg(grant_of=lambda r, g: W.encode_grant(oid, ts, th, configstamp=3)),
+        "grant_oid_non_ascii": msg(grant_of=lambda r, g: W.encode_grant(oid + "é", ts, th)),
+        "grant_hash_non_ascii": msg(grant_of=lambda r, g: W.encode_grant(oid, ts, th[:-1] + "é")),
+        "grant_reordered": msg(grant_of=lambda r, g: _reorder(g)),
+        "grant_200_bytes": msg(grant_of=lambda r, g: W.encode_grant(oid + "o" * 40, ts, th)),
+        "key_bad_utf8": _bad_key_byte(msg(), oid),
+        # the first MultiGrant names the grant key twice: LinkedHashMap keeps the first
+        # position and the LAST value (a variant: another transaction hash), while every
+        # other MultiGrant carries the first value's bytes -- they must not take the
+        # variant's prep results
+        "repeated_key_first_mg": msg(grant_of=lambda r, g: [(oid, g), (oid, W.encode_grant(oid, ts, th_alt))]
+                                     if r == r0 else g),
+    }
+
+
+def test_wire_layout_matcher_edges(pool4):
+    """Decode arrays and verdicts == oracle for every form around the layout matcher's
+    edges (and the walk it falls back to), at every message alignment."""
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 16, first_cert=5150, faults=False)
+    ids4 = W.SERVER_IDS[:4]
+    msgs, kinds, hashes = [], [], []
+    for c in range(0, 16, 4):
+        forms = _matcher_forms(s, c, ids4)
+        for kind, m in forms.items():
+            msgs.append(m)
+            kinds.append(kind)
+            hashes.append(s.batch.expected_hash[c])
+    ids, off = W.server_id_table(4)
+    for pad in (1, 3):
+        wb = _pack(msgs, pad=pad)
+        wb.expected_hash = np.stack(hashes)
+        d = ver.decode_write2(wb)
+        o = O.w2_decode(wb, ids, off)
+        assert_decode_equal(d, o, f"matcher forms pad={pad}")
+        for strict in (True, False):
+            g, st = ver.verify_write2(wb, 4, strict)
+            ov, ost = O.verify_write2(pool4.moduli, ids, off, wb, 4, strict)
+            np.testing.assert_array_equal(st, ost)
+            np.testing.assert_array_equal(g.cert_reason, ov.cert_reason, err_msg=str(list(zip(kinds, g.cert_reason))))
+            np.testing.assert_array_equal(g.cert_accept_bits, ov.cert_accept_bits)
+    # (the last verify ran with strict = False: three valid grants of four are a quorum)
+    kinds = np.array(kinds)
+    acc = {k: g.cert_accept[kinds == k] for k in set(kinds.tolist())}
+    for k in ("plain", "key_60", "key_61", "key_non_ascii", "trailing_unknown", "grant_reordered",
+              "repeated_key_first_mg"):  # the last: the three other MultiGrants carry the signed bytes
+        assert acc[k].all(), (k, g.cert_reason[kinds == k])
+    for k in ("sig_under_other_key", "sig_255", "key_bad_utf8", "grant_200_bytes"):
+        assert not acc[k].any(), k
+    ver.close()
