@@ -61,7 +61,7 @@ struct W2Args {
 // level 1's entry records + the packed per-message counts and their scan.
 constexpr uint32_t kW2MaxCertEntries = 32;
 constexpr int kW2MsgArrays = 13;
-constexpr int kW2CeArrays = 12;
+constexpr int kW2CeArrays = 11;
 // Level 1 records the key / value slices of a message's first kW2InlEntries
 // certificate entries, so the compact entry list is copied, not re-parsed.
 constexpr uint32_t kW2InlEntries = 4;

@@ -605,6 +605,73 @@ __device__ uint32_t msg_level(ByteReader& r, uint32_t& nce, uint32_t& nops, uint
   return rc < 0 ? kStMal : 0u;
 }
 
+__device__ __forceinline__ uint32_t wbyte(const uint32_t* w, uint32_t k) {  // k compile-time after unrolling
+  return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+}
+
+// bytes [a, b) of a window, as a mask of word t
+__device__ __forceinline__ uint32_t span_mask(int t, int a, int b) {
+  const int lo = a - 4 * t, hi = b - 4 * t;
+  const uint32_t m_hi = hi >= 4 ? ~0u : hi <= 0 ? 0u : (1u << (8 * hi)) - 1u;
+  const uint32_t m_lo = lo <= 0 ? 0u : lo >= 4 ? ~0u : (1u << (8 * lo)) - 1u;
+  return m_hi & ~m_lo;
+}
+
+// The first grant of a MultiGrant value, as first_grant finds it, from its
+// first 16 bytes `h` (at `off`) and one word: lengths of one or two varint
+// bytes, a key < 128 bytes (otherwise none -- the match is a hint, and only
+// equal bytes use it).  ref_head parses the window: the grant's slice and the
+// word expected at `gpos` (its tag and length); ref_grant_win loads both.
+struct RefHead {
+  uint32_t off, len, gpos, word, mask;
+  bool ok;
+};
+__device__ __forceinline__ RefHead ref_head(const uint32_t (&h)[4], uint32_t off, uint32_t len) {
+  RefHead g{~0u, 0, 0, 0, 0, false};
+  const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
+  uint32_t n1, L1, et, kl;
+  if (c1 < 0x80u) {
+    n1 = 1;
+    L1 = c1;
+    et = c2;
+    kl = wbyte(h, 3);
+  } else if (c2 < 0x80u) {
+    n1 = 2;
+    L1 = (c1 & 0x7Fu) | (c2 << 7);
+    et = wbyte(h, 3);
+    kl = wbyte(h, 4);
+  } else {
+    return g;
+  }
+  const uint32_t e1 = off + 1 + n1;
+  if (len < 8 || wbyte(h, 0) != 0x0Au || et != 0x0Au || kl >= 0x80u || e1 + L1 > off + len || L1 < kl + 3 + 1 + 3)
+    return g;
+  const uint32_t rest = L1 - 3 - kl;  // gl + its varint
+  if (rest == 129) return g;         // gl = 127 in two bytes
+  const uint32_t n2 = rest <= 128 ? 1u : 2u, gl = rest - n2;
+  g.gpos = e1 + 2 + kl;  // gpos + 4 <= the grant's end (gl >= 3)
+  g.off = g.gpos + 1 + n2;
+  g.len = gl;
+  g.word = n2 == 1 ? 0x12u | (gl << 8) : 0x12u | (((gl & 0x7Fu) | 0x80u) << 8) | ((gl >> 7) << 16);
+  g.mask = n2 == 1 ? 0xFFFFu : 0xFFFFFFu;
+  g.ok = true;
+  return g;
+}
+
+__device__ __forceinline__ RefGrant ref_grant_win(ByteReader& r, uint32_t off, uint32_t len) {
+  RefGrant g;
+  if (len < 8) return g;
+  uint32_t h[4];
+  window16(r.base, r.len, off, h);
+  const RefHead rh = ref_head(h, off, len);
+  if (rh.ok && (ld4(r.base, rh.gpos) & rh.mask) == rh.word) {
+    g.off = rh.off;
+    g.len = rh.len;
+  }
+  return g;
+}
+
+
 // One walk of a MultiGrant value: validates it as valid_multigrant does,
 // counts its grants / grantSignatures entries on the wire, and records what
 // the decode of the common shape needs -- the last entry of each map (its key
@@ -668,18 +735,9 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
 #ifndef MOCHI_W2_MATCH
 #define MOCHI_W2_MATCH 1  // A/B: 0 = every MultiGrant through valid_mg_scan
 #endif
-
-__device__ __forceinline__ uint32_t wbyte(const uint32_t* w, uint32_t k) {  // k compile-time after unrolling
-  return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-}
-
-// bytes [a, b) of a window, as a mask of word t
-__device__ __forceinline__ uint32_t span_mask(int t, int a, int b) {
-  const int lo = a - 4 * t, hi = b - 4 * t;
-  const uint32_t m_hi = hi >= 4 ? ~0u : hi <= 0 ? 0u : (1u << (8 * hi)) - 1u;
-  const uint32_t m_lo = lo <= 0 ? 0u : lo >= 4 ? ~0u : (1u << (8 * lo)) - 1u;
-  return m_hi & ~m_lo;
-}
+#ifndef MOCHI_W2_GWIN_SEQ
+#define MOCHI_W2_GWIN_SEQ 0
+#endif
 
 // The common Grant shape, canonical and valid (ASCII strings), from its own
 // windows: `hib` = bytes with the high bit set over the whole grant, w0 = its
@@ -730,13 +788,17 @@ __device__ __forceinline__ bool grant_match(const uint8_t* base, uint32_t mlen, 
 
 // kw / sw (out): the windows at the grants entry (0x0A kl key) and at the
 // serverId (0x22 sl serverId), for the signer and key-slot lookups
-__device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, const RefGrant ref, MGScan& m, uint32_t (&kw)[16],
-                         uint32_t (&sw)[16]) {
+// (rvo, rvl): the message's first certificate entry's value (ref_head: the grant
+// the prep hint compares with), ~0 = this is that entry
+__device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, uint32_t rvo, uint32_t rvl, MGScan& m,
+                         uint32_t (&kw)[16], uint32_t (&sw)[16]) {
   const uint8_t* base = r.base;
   const uint32_t mlen = r.len;
   if (vl < 272) return false;
-  uint32_t h[4];
+  uint32_t h[4], rh[4] = {0u, 0u, 0u, 0u};
   window16(base, mlen, vo, h);
+  if (rvo != ~0u && rvl >= 8) window16(base, mlen, rvo, rh);  // beside this value's header
+  const RefHead ref = rvo != ~0u ? ref_head(rh, rvo, rvl) : RefHead{~0u, 0, 0, 0, 0, false};
   const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
   uint32_t n1, L1, et, kl;
   if (c1 < 0x80u) {
@@ -764,6 +826,8 @@ __device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, const RefGrant
   if (gl > 192) return false;
   // ---- independent loads: framing words, key / serverId windows, the grant ----
   const uint32_t gh = ld4(base, gpos), t5 = ld4(base, p5), sh = ld4(base, end - 259);
+  const bool cmp = ref.ok && ref.len == gl;  // the first grant's header word is checked below
+  const uint32_t rgh = cmp ? ld4(base, ref.gpos) : 0u;
   uint32_t(&k1)[16] = kw;
   uint32_t k4[16];
   window64(base, mlen, e1, k1);      // 0x0A kl key
@@ -783,9 +847,12 @@ __device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, const RefGrant
   }
   ok = ok && kdiff == 0 && (hi & 0x80808080u) == 0;
   // ---- the grant: its high-bit count, its first window, and the compare with the reference grant ----
-  const bool cmp = ref.off != ~0u && ref.len == gl;
   uint32_t w0[16], hib = 0, gdiff = 0;
+#if MOCHI_W2_GWIN_SEQ  // A/B: the grant's windows one after the other (fewer registers, two more latencies)
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
   for (int c = 0; c < 3; c++) {
     if (64u * c < gl) {
       uint32_t w[16], v[16];
@@ -807,7 +874,7 @@ __device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, const RefGrant
   m.sid_off = s_tag + 2;
   m.sid_len = sl;
   m.first_nc = false;
-  m.same = cmp && gdiff == 0;
+  m.same = cmp && gdiff == 0 && (rgh & ref.mask) == ref.word;
   m.sig_key = true;
   return true;
 }
@@ -1015,71 +1082,22 @@ __device__ __forceinline__ uint8_t slot_from_window(ByteReader& r, const W2Msg& 
   return slot;
 }
 
-// The first grant of a MultiGrant value, as first_grant finds it, from one
-// window and one word (lengths of one or two varint bytes, a key < 128 bytes:
-// otherwise none -- the match is a hint, and only equal bytes use it).
-__device__ __forceinline__ RefGrant ref_grant_win(ByteReader& r, uint32_t off, uint32_t len) {
-  RefGrant g;
-  if (len < 8) return g;
-  uint32_t h[4];
-  window16(r.base, r.len, off, h);
-  const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
-  uint32_t n1, L1, et, kl;
-  if (c1 < 0x80u) {
-    n1 = 1;
-    L1 = c1;
-    et = c2;
-    kl = wbyte(h, 3);
-  } else if (c2 < 0x80u) {
-    n1 = 2;
-    L1 = (c1 & 0x7Fu) | (c2 << 7);
-    et = wbyte(h, 3);
-    kl = wbyte(h, 4);
-  } else {
-    return g;
-  }
-  const uint32_t e1 = off + 1 + n1;
-  if (wbyte(h, 0) != 0x0Au || et != 0x0Au || kl >= 0x80u || e1 + L1 > off + len || L1 < kl + 3 + 1 + 3) return g;
-  const uint32_t rest = L1 - 3 - kl;
-  if (rest == 129) return g;
-  const uint32_t n2 = rest <= 128 ? 1u : 2u, gl = rest - n2, gpos = e1 + 2 + kl;
-  const uint32_t gh = ld4(r.base, gpos);  // gpos + 4 <= the grant's end (gl >= 3)
-  const bool ok = (gh & 0xFFu) == 0x12u &&
-                  (n2 == 1 ? ((gh >> 8) & 0xFFu) == gl : ((gh >> 8) & 0xFFFFu) == (((gl & 0x7Fu) | 0x80u) | ((gl >> 7) << 8)));
-  if (ok) {
-    g.off = gpos + 1 + n2;
-    g.len = gl;
-  }
-  return g;
-}
-
 // Certificate entries (compact, in wire order per message): message index,
-// key and value slices (message-relative), the key's last four bytes (all of
-// it, zero-padded, when shorter: k_w2_mg's sibling filter), the index of the
-// entry holding the key's final value (~0 unless this entry is the key's
-// first), and the number of distinct grants of a final-value entry.
+// key and value slices (message-relative), the index of the entry holding the
+// key's final value (~0 unless this entry is the key's first), and the number
+// of distinct grants of a final-value entry.
 // A decoded MultiGrant with one distinct grant (the common shape) also leaves
 // its emit record here -- grant value slice, signature offset (message-
 // relative, ~0 = none), signer << 8 | key slot -- written by k_w2_mg while the
 // bytes are hot, so k_w2_emit_mg need not walk it again.
 struct CE {
   uint32_t *msg, *koff, *klen, *voff, *vlen, *last, *ng;
-  uint32_t *r_goff, *r_glen, *r_sig, *r_sk, *ktail;
+  uint32_t *r_goff, *r_glen, *r_sig, *r_sk;
 };
 static_assert(sizeof(CE) == kW2CeArrays * sizeof(uint32_t*), "kW2CeArrays (w2.h) counts the CE arrays");
 __host__ __device__ inline CE ce_view(uint32_t* p, uint32_t cap) {
   const size_t c = cap;
-  return CE{p,         p + c,     p + 2 * c, p + 3 * c, p + 4 * c,  p + 5 * c,
-            p + 6 * c, p + 7 * c, p + 8 * c, p + 9 * c, p + 10 * c, p + 11 * c};
-}
-
-// the last four bytes of key [ko, ko + kl) of the message, little-endian (the
-// whole key, zero-padded, when it is shorter)
-__device__ __forceinline__ uint32_t key_tail(ByteReader& r, uint32_t ko, uint32_t kl) {
-  if (kl >= 4) return ld4(r.base, ko + kl - 4);
-  uint32_t v = 0;
-  for (uint32_t j = 0; j < kl; j++) v |= r.at(ko + j) << (8 * j);
-  return v;
+  return CE{p, p + c, p + 2 * c, p + 3 * c, p + 4 * c, p + 5 * c, p + 6 * c, p + 7 * c, p + 8 * c, p + 9 * c, p + 10 * c};
 }
 
 // The distinct grants of one decoded MultiGrant value [mo, mo+ml), in map
@@ -1208,9 +1226,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOCHI_W2MSG
   }
   ByteReader r;
   r.init(wire + moff[m], mlen[m]);
-  uint32_t nce, nops, wo = 0, wl = 0, to = 0, tl = 0;
-  const uint32_t bits =
-      msg_level(r, nce, nops, wo, wl, to, tl, s.inl + (size_t)4 * kW2InlEntries * m, s.inl_ops + (size_t)2 * kW2InlOps * m);
+  uint32_t nce = 0, nops = 0, wo = 0, wl = 0, to = 0, tl = 0;
+  uint32_t* inl = s.inl + (size_t)4 * kW2InlEntries * m;
+  uint32_t* inl_ops = s.inl_ops + (size_t)2 * kW2InlOps * m;
+  const uint32_t bits = msg_level(r, nce, nops, wo, wl, to, tl, inl, inl_ops);
   if (bits) nce = nops = 0;
   s.cnt_ce[m] = nce;
   s.cnt_o[m] = nops;
@@ -1229,8 +1248,6 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
   const uint32_t nce = s.cnt_ce[m];
   if (nce == 0) return;
   uint32_t e = s.ce_base[m];
-  ByteReader r;
-  r.init(wire + moff[m], mlen[m]);
   if (nce <= kW2InlEntries) {  // recorded by level 1: copy
     const uint4* q = (const uint4*)(s.inl + (size_t)4 * kW2InlEntries * m);
 #pragma unroll 4
@@ -1241,10 +1258,11 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
       ce.klen[e] = v.y;
       ce.voff[e] = v.z;
       ce.vlen[e] = v.w;
-      ce.ktail[e] = key_tail(r, v.x, v.y);
     }
     return;
   }
+  ByteReader r;
+  r.init(wire + moff[m], mlen[m]);
   uint32_t pos = s.wc_off[m];
   const uint32_t end = pos + s.wc_len[m];
   Fld f;
@@ -1258,7 +1276,6 @@ __global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ 
     ce.klen[e] = x.klen;
     ce.voff[e] = x.voff;
     ce.vlen[e] = x.vlen;
-    ce.ktail[e] = key_tail(r, x.koff, x.klen);
     e++;
   }
 }
@@ -1348,27 +1365,22 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
     const uint32_t m = ce.msg[e];
     ByteReader r;
     r.init(wire + moff[m], mlen[m]);
-    const uint32_t b0 = s.ce_base[m], b1 = s.ce_base[m + 1], ko = ce.koff[e], kl = ce.klen[e], kt = ce.ktail[e];
+    const uint32_t b0 = s.ce_base[m], b1 = s.ce_base[m + 1], ko = ce.koff[e], kl = ce.klen[e];
     bool first = true;
     uint32_t last = e;
-    // siblings with this key: length and last four bytes from the entry list (a
-    // key of at most four bytes is all in them), the bytes compared only then
-#pragma unroll 4
-    for (uint32_t j = b0; j < b1; j++) {
-      if (j == e || ce.klen[j] != kl || ce.ktail[j] != kt) continue;
-      if (kl > 4 && !key_eq(r, ce.koff[j], kl, ko, kl)) continue;
-      if (j < e) first = false;
-      else last = j;
-    }
+#pragma unroll 1
+    for (uint32_t j = b0; j < b1; j++)
+      if (j != e && key_eq(r, ce.koff[j], ce.klen[j], ko, kl)) {
+        if (j < e) first = false;
+        else last = j;
+      }
     const uint32_t vo = ce.voff[e], vl = ce.vlen[e];
     uint32_t bits = 0, ng = 0;
     MGScan sc;
     // the R MultiGrants of an honest certificate carry the same grant bytes:
     // a grant equal to the first MultiGrant's first grant is parsed by that
     // entry's lane only
-    const RefGrant ref = e == b0                ? RefGrant{}
-                         : MOCHI_W2_MATCH ? ref_grant_win(r, ce.voff[b0], ce.vlen[b0])
-                                          : first_grant(r, ce.voff[b0], ce.vlen[b0]);
+    const uint32_t rvo = e == b0 ? ~0u : ce.voff[b0], rvl = e == b0 ? 0u : ce.vlen[b0];
     // the emit record, read by k_w2_emit_mg when ng == 1
     auto rec = [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
       ce.r_goff[e] = go;
@@ -1378,8 +1390,14 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
     };
     stp.mark(1);
     uint32_t kw[16], sw[16];
-    const bool fast = MOCHI_W2_MATCH && mg_match(r, vo, vl, ref, sc, kw, sw);
-    const bool valid = fast || valid_mg_scan(r, vo, vl, sc, ref);
+    const bool fast = MOCHI_W2_MATCH && mg_match(r, vo, vl, rvo, rvl, sc, kw, sw);
+    bool valid = fast;
+    if (!fast) {
+      const RefGrant ref = rvo == ~0u     ? RefGrant{}
+                           : MOCHI_W2_MATCH ? ref_grant_win(r, rvo, rvl)
+                                            : first_grant(r, rvo, rvl);
+      valid = valid_mg_scan(r, vo, vl, sc, ref);
+    }
     stp.mark(2);
     if (valid && e == b0 && sc.first_nc) bits |= kStFirstNC;  // the reference grant of this message's other lanes
     if (!valid) {

@@ -599,7 +599,7 @@ def _matcher_forms(s, c, ids):
     th_alt = th[:-1] + ("0" if th[-1] != "0" else "1")
 
     def msg(grant_of=lambda r, g: g, key_of=lambda r, o: o, sig_key_of=None, sid_of=lambda r: ids[r],
-            sig_of=lambda r, sg: sg, extra_of=None, op_key=None):
+            sig_of=lambda r, sg: sg, extra_of=None, ops_of=None, cert_key_of=lambda r: ids[r], dup_entry=False):
         ent = []
         for r, o, g, sg in items:
             k = key_of(r, o)
@@ -607,8 +607,11 @@ def _matcher_forms(s, c, ids):
             gl = grant_of(r, g)
             grants = gl if isinstance(gl, list) else [(k, gl)]
             mg = W.encode_multigrant(grants, sid_of(r), "", "", [(sk, sig_of(r, sg))])
-            ent.append((ids[r], mg + (extra_of(r) if extra_of else b"")))
-        return W.encode_write2(ent, [W.encode_operation(2, op_key if op_key is not None else key_of(r0, oid))])
+            ent.append((cert_key_of(r), mg + (extra_of(r) if extra_of else b"")))
+        if dup_entry:
+            ent.append(ent[0])  # a repeated certificate key: first position, last value
+        key = key_of(r0, oid)
+        return W.encode_write2(ent, ops_of(key) if ops_of else [W.encode_operation(2, key)])
 
     return {
         "plain": msg(),
@@ -632,6 +635,17 @@ def _matcher_forms(s, c, ids):
         "grant_reordered": msg(grant_of=lambda r, g: _reorder(g)),
         "grant_200_bytes": msg(grant_of=lambda r, g: W.encode_grant(oid + "o" * 40, ts, th)),
         "key_bad_utf8": _bad_key_byte(msg(), oid),
+        # level-1 shapes: operations, certificate keys
+        "op_no_action": msg(ops_of=lambda k: [W.encode_operation(0, k)]),
+        "op_operand2": msg(ops_of=lambda k: [W.encode_operation(2, k, "v")]),
+        "ops_4": msg(ops_of=lambda k: [W.encode_operation(2, k + str(i) if i else k) for i in range(4)]),
+        "ops_5": msg(ops_of=lambda k: [W.encode_operation(2, k + str(i) if i else k) for i in range(5)]),
+        "op_second_names_key": msg(ops_of=lambda k: [W.encode_operation(2, k + "z"), W.encode_operation(2, k)]),
+        "op_key_57": msg(key_of=lambda r, o: (o + "-" + "q" * 57)[:57]),
+        "cert_key_non_ascii": msg(cert_key_of=lambda r: ids[r] + "é"),
+        "cert_key_57": msg(cert_key_of=lambda r: (ids[r] + "-" + "c" * 57)[:57]),
+        "cert_key_repeated": msg(dup_entry=True),
+        "cert_keys_equal_pairs": msg(cert_key_of=lambda r: ids[r % 2]),
         # the first MultiGrant names the grant key twice: LinkedHashMap keeps the first
         # position and the LAST value (a variant: another transaction hash), while every
         # other MultiGrant carries the first value's bytes -- they must not take the
@@ -671,6 +685,7 @@ def test_wire_layout_matcher_edges(pool4):
     kinds = np.array(kinds)
     acc = {k: g.cert_accept[kinds == k] for k in set(kinds.tolist())}
     for k in ("plain", "key_60", "key_61", "key_non_ascii", "trailing_unknown", "grant_reordered",
+              "op_operand2", "op_key_57", "cert_key_non_ascii", "cert_key_57", "cert_key_repeated",
               "repeated_key_first_mg"):  # the last: the three other MultiGrants carry the signed bytes
         assert acc[k].all(), (k, g.cert_reason[kinds == k])
     for k in ("sig_under_other_key", "sig_255", "key_bad_utf8", "grant_200_bytes"):
