@@ -652,6 +652,15 @@ static bool dedup_off() {
   return off;
 }
 
+// MOCHI_PREP_FIRST=1 (A/B): grant prep ahead of k_rsa_pow on the main stream
+static bool prep_first() {
+  static const bool on = [] {
+    const char* e = getenv("MOCHI_PREP_FIRST");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 hipError_t launch_withhold(const uint8_t* flags, uint32_t n, uint8_t* sig, uint32_t* rejected, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_withhold, dim3(cdiv(n, 256)), dim3(256), 0, st, flags, n, sig, rejected);
   return hipGetLastError();
@@ -681,48 +690,73 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   const bool prep = N && !a.skip_prep_tally;
   const bool fork = prep && a.aux;
   hipStream_t ps = fork ? a.aux : st;
-  mark(kStageBucket, false, st);
-  if (N) {
-    hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, st);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(a.perm, 0xFF, sizeof(uint32_t) * (size_t)a.n_slots, st);
-    if (e != hipSuccess) return e;
-    const uint32_t lds = sizeof(uint32_t) * a.n_keys;
-    const uint32_t cblocks = cdiv(N, 256) < 1024 ? cdiv(N, 256) : 1024;
-    hipLaunchKernelGGL(k_bucket_count, dim3(cblocks), dim3(256), lds, st, a.signer, N, a.n_keys, a.count);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, a.count, a.n_keys, a.cursor, a.total);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(cdiv(N, 256 * kScatterPer)), dim3(256), 2 * lds, st, a.signer, N, a.n_keys, a.cursor,
-                       a.perm);
-  }
-  mark(kStageBucket, true, st);
-  if (fork) {
+  auto bucket = [&](hipStream_t bs) -> hipError_t {
+    mark(kStageBucket, false, bs);
+    if (N) {
+      hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, bs);
+      if (e != hipSuccess) return e;
+      e = hipMemsetAsync(a.perm, 0xFF, sizeof(uint32_t) * (size_t)a.n_slots, bs);
+      if (e != hipSuccess) return e;
+      const uint32_t lds = sizeof(uint32_t) * a.n_keys;
+      const uint32_t cblocks = cdiv(N, 256) < 1024 ? cdiv(N, 256) : 1024;
+      hipLaunchKernelGGL(k_bucket_count, dim3(cblocks), dim3(256), lds, bs, a.signer, N, a.n_keys, a.count);
+      hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, bs, a.count, a.n_keys, a.cursor, a.total);
+      hipLaunchKernelGGL(k_bucket_scatter, dim3(cdiv(N, 256 * kScatterPer)), dim3(256), 2 * lds, bs, a.signer, N,
+                         a.n_keys, a.cursor, a.perm);
+    }
+    mark(kStageBucket, true, bs);
+    return hipSuccess;
+  };
+  auto grant_prep = [&](hipStream_t ps) -> hipError_t {
+    mark(kStagePrep, false, ps);
+    if (prep) {
+      if (a.rare && a.cert_grant_off && C && !dedup_off()) {
+        const PrepCertArgs pc{a.grant_key, a.cert_grant_off, a.grant_same, C, a.rare};
+        hipError_t e = hipMemsetAsync(a.rare, 1, N, ps);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_grant_prep_cert, dim3(cdiv(C, 256)), dim3(256), 0, ps, pa, pc);
+        hipLaunchKernelGGL(k_grant_prep_rare, dim3(cdiv(N, kRareSpan)), dim3(256), 0, ps, pa, (const uint8_t*)a.rare);
+      } else {
+        hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
+      }
+    }
+    mark(kStagePrep, true, ps);
+    return hipSuccess;
+  };
+  if (fork && prep_first()) {
+    // A/B (MOCHI_PREP_FIRST=1): prep on the main stream ahead of pow, the short
+    // bucket kernels beside it on the aux stream
     hipError_t e = hipEventRecord(a.ev_fork, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(a.aux, a.ev_fork, 0);
+    if (e == hipSuccess) e = bucket(a.aux);
+    if (e == hipSuccess) e = hipEventRecord(a.ev_join, a.aux);
+    if (e == hipSuccess) e = grant_prep(st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, a.ev_join, 0);
     if (e != hipSuccess) return e;
-  }
-  mark(kStagePrep, false, ps);
-  if (prep) {
-    if (a.rare && a.cert_grant_off && C && !dedup_off()) {
-      const PrepCertArgs pc{a.grant_key, a.cert_grant_off, a.grant_same, C, a.rare};
-      hipError_t e = hipMemsetAsync(a.rare, 1, N, ps);
+    mark(kStagePow, false, st);
+    if (N) launch_rsa_pow(a, st);
+    mark(kStagePow, true, st);
+  } else {
+    hipError_t e = bucket(st);
+    if (e != hipSuccess) return e;
+    if (fork) {
+      e = hipEventRecord(a.ev_fork, st);
+      if (e == hipSuccess) e = hipStreamWaitEvent(a.aux, a.ev_fork, 0);
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(k_grant_prep_cert, dim3(cdiv(C, 256)), dim3(256), 0, ps, pa, pc);
-      hipLaunchKernelGGL(k_grant_prep_rare, dim3(cdiv(N, kRareSpan)), dim3(256), 0, ps, pa, (const uint8_t*)a.rare);
-    } else {
-      hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
     }
-  }
-  mark(kStagePrep, true, ps);
-  if (fork) {
-    hipError_t e = hipEventRecord(a.ev_join, a.aux);
+    e = grant_prep(ps);
     if (e != hipSuccess) return e;
-  }
-  mark(kStagePow, false, st);
-  if (N) launch_rsa_pow(a, st);
-  mark(kStagePow, true, st);
-  if (fork) {
-    hipError_t e = hipStreamWaitEvent(st, a.ev_join, 0);
-    if (e != hipSuccess) return e;
+    if (fork) {
+      e = hipEventRecord(a.ev_join, a.aux);
+      if (e != hipSuccess) return e;
+    }
+    mark(kStagePow, false, st);
+    if (N) launch_rsa_pow(a, st);
+    mark(kStagePow, true, st);
+    if (fork) {
+      e = hipStreamWaitEvent(st, a.ev_join, 0);
+      if (e != hipSuccess) return e;
+    }
   }
   mark(kStageFinal, false, st);
   if (N) {

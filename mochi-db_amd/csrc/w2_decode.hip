@@ -735,9 +735,6 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
 #ifndef MOCHI_W2_MATCH
 #define MOCHI_W2_MATCH 1  // A/B: 0 = every MultiGrant through valid_mg_scan
 #endif
-#ifndef MOCHI_W2_GWIN_SEQ
-#define MOCHI_W2_GWIN_SEQ 0
-#endif
 
 // The common Grant shape, canonical and valid (ASCII strings), from its own
 // windows: `hib` = bytes with the high bit set over the whole grant, w0 = its
@@ -848,11 +845,7 @@ __device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, uint32_t rvo, 
   ok = ok && kdiff == 0 && (hi & 0x80808080u) == 0;
   // ---- the grant: its high-bit count, its first window, and the compare with the reference grant ----
   uint32_t w0[16], hib = 0, gdiff = 0;
-#if MOCHI_W2_GWIN_SEQ  // A/B: the grant's windows one after the other (fewer registers, two more latencies)
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
   for (int c = 0; c < 3; c++) {
     if (64u * c < gl) {
       uint32_t w[16], v[16];
