@@ -4,7 +4,7 @@
     python scripts/pmc_summary.py --round r01
 
 Reads gpurun_out/pmc/<pass>/run_counter_collection.csv (scripts/pmc.sh) and
-gpurun_out/prof_kt/run_kernel_stats.csv (scripts/gpu_round.sh), writes
+gpurun_out/prof_kt/run_kernel_stats.csv (`scripts/gpu.sh kt`), writes
 profiles/<round>_pmc_summary.json, profiles/<round>_kernel_stats.csv and
 profiles/pmc_rsa_pow.json (read by bench.py for roofline.traffic).
 
