@@ -735,6 +735,12 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
 #ifndef MOCHI_W2_MATCH
 #define MOCHI_W2_MATCH 1  // A/B: 0 = every MultiGrant through valid_mg_scan
 #endif
+#ifndef MOCHI_W2_SPLIT
+#define MOCHI_W2_SPLIT 0
+#endif
+#ifndef MOCHI_W2_REFCMP
+#define MOCHI_W2_REFCMP 1  // A/B: 0 = the matcher leaves the compare with the first grant to prep
+#endif
 
 // The common Grant shape, canonical and valid (ASCII strings), from its own
 // windows: `hib` = bytes with the high bit set over the whole grant, w0 = its
@@ -794,8 +800,8 @@ __device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, uint32_t rvo, 
   if (vl < 272) return false;
   uint32_t h[4], rh[4] = {0u, 0u, 0u, 0u};
   window16(base, mlen, vo, h);
-  if (rvo != ~0u && rvl >= 8) window16(base, mlen, rvo, rh);  // beside this value's header
-  const RefHead ref = rvo != ~0u ? ref_head(rh, rvo, rvl) : RefHead{~0u, 0, 0, 0, 0, false};
+  if (MOCHI_W2_REFCMP && rvo != ~0u && rvl >= 8) window16(base, mlen, rvo, rh);  // beside this value's header
+  const RefHead ref = MOCHI_W2_REFCMP && rvo != ~0u ? ref_head(rh, rvo, rvl) : RefHead{~0u, 0, 0, 0, 0, false};
   const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
   uint32_t n1, L1, et, kl;
   if (c1 < 0x80u) {
@@ -845,12 +851,16 @@ __device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, uint32_t rvo, 
   ok = ok && kdiff == 0 && (hi & 0x80808080u) == 0;
   // ---- the grant: its high-bit count, its first window, and the compare with the reference grant ----
   uint32_t w0[16], hib = 0, gdiff = 0;
+  uint32_t ga = g0, ra = ref.off;
+#if MOCHI_W2_SPLIT  // A/B: the grant's windows only after the key / serverId windows are reduced (fewer registers)
+  asm volatile("" : "+v"(ga), "+v"(ra) : "v"(kdiff | hi));
+#endif
 #pragma unroll
   for (int c = 0; c < 3; c++) {
     if (64u * c < gl) {
       uint32_t w[16], v[16];
-      window64(base, mlen, g0 + 64 * c, w);
-      if (cmp) window64(base, mlen, ref.off + 64 * c, v);
+      window64(base, mlen, ga + 64 * c, w);
+      if (cmp) window64(base, mlen, ra + 64 * c, v);
 #pragma unroll
       for (int t = 0; t < 16; t++) {
         const uint32_t mk = span_mask(t, 0, (int)gl - 64 * c);
