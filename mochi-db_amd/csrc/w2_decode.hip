@@ -685,6 +685,8 @@ struct MGScan {
   bool first_nc;             // the first grants entry holds one value, parsed and not canonical
   bool same;                 // the grant's bytes equal the reference grant's (prep reuses its results)
   bool sig_key;              // mg_match: the signature entry's key is the grant's
+  uint16_t signer;           // mg_match (MOCHI_W2_EARLY): the signer and key slot of the grant
+  uint8_t slot;
 };
 
 __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan& m, const RefGrant ref = RefGrant{}) {
@@ -716,171 +718,6 @@ __device__ bool valid_mg_scan(ByteReader& r, uint32_t off, uint32_t len, MGScan&
   return rc == 0;
 }
 
-// ---- the reference encoder's MultiGrant, matched from a few wide loads ------
-// encode_multigrant / protobuf-java (MochiProtocol.proto:117-124 + field 5):
-// one grant, fields in number order, each map entry its key then its value,
-//   0x0A L1 { 0x0A kl key 0x12 gl Grant } 0x22 sl serverId
-//   0x2A L5 { 0x0A kl key 0x12 0x80 0x02 signature[256] }
-// the signature entry under the grant's key, key and serverId ASCII (kl, sl <= 60),
-// L1 and gl one or two varint bytes, and the Grant itself in its common
-// canonical shape 0x0A L objectId 0x10 ts 0x22 H transactionHash (<= 192 bytes,
-// ASCII strings).  Every position follows from the first 16 bytes (the
-// signature entry's from the value's end), so the loads after the first are
-// independent of each other -- three load latencies (header, windows, the
-// grant's timestamp) where the walk (next_fld / ByteReader::at) paid one per
-// field, length and word.  Any difference returns false and valid_mg_scan
-// decides; what this accepts, valid_mg_scan accepts with the same MGScan (one
-// grants and one grantSignatures entry of one key and one value each, the grant
-// parsed and canonical -- parse_grant_t's CANON rules).
-#ifndef MOCHI_W2_MATCH
-#define MOCHI_W2_MATCH 1  // A/B: 0 = every MultiGrant through valid_mg_scan
-#endif
-#ifndef MOCHI_W2_SPLIT
-#define MOCHI_W2_SPLIT 0
-#endif
-#ifndef MOCHI_W2_REFCMP
-#define MOCHI_W2_REFCMP 1  // A/B: 0 = the matcher leaves the compare with the first grant to prep
-#endif
-
-// The common Grant shape, canonical and valid (ASCII strings), from its own
-// windows: `hib` = bytes with the high bit set over the whole grant, w0 = its
-// first 16 bytes, read from the timestamp's tag on with one more window.
-__device__ __forceinline__ bool grant_match(const uint8_t* base, uint32_t mlen, uint32_t g0, uint32_t gl,
-                                            const uint32_t (&w0)[16], uint32_t hib) {
-  const uint32_t L = wbyte(w0, 1);
-  if (wbyte(w0, 0) != 0x0Au || L == 0 || L >= 0x80u || L + 6 > gl) return false;
-  uint32_t tb[4];
-  window16(base, mlen, g0 + 2 + L, tb);
-  if (wbyte(tb, 0) != 0x10u) return false;
-  // timestamp: 1..9 varint bytes, minimal (nonzero last byte; a one-byte 0 is the default, never written)
-  uint32_t k = 0, last = 0;
-  bool end = false;
-#pragma unroll
-  for (uint32_t i = 1; i <= 9; i++) {
-    const uint32_t c = wbyte(tb, i);
-    if (!end) {
-      k = i;
-      last = c;
-      end = c < 0x80u;
-    }
-  }
-  if (!end || last == 0) return false;
-  uint32_t c1 = 0, c2 = 0, tag = 0;  // the bytes after the timestamp (k + 1 <= 10)
-#pragma unroll
-  for (uint32_t i = 2; i <= 10; i++) {
-    if (i == k + 1) {
-      tag = wbyte(tb, i);
-      c1 = wbyte(tb, i + 1);
-      c2 = wbyte(tb, i + 2);
-    }
-  }
-  if (tag != 0x22u) return false;
-  uint32_t hl, nh;
-  if (c1 < 0x80u) {
-    hl = c1;
-    nh = 1;
-  } else if (c2 < 0x80u && c2 != 0) {
-    hl = (c1 & 0x7Fu) | (c2 << 7);
-    nh = 2;
-  } else {
-    return false;
-  }
-  const uint32_t hp = 2 + L + 1 + k + 1 + nh;
-  return hl != 0 && hp + hl == gl && hib == (k - 1) + (nh - 1);
-}
-
-// kw / sw (out): the windows at the grants entry (0x0A kl key) and at the
-// serverId (0x22 sl serverId), for the signer and key-slot lookups
-// (rvo, rvl): the message's first certificate entry's value (ref_head: the grant
-// the prep hint compares with), ~0 = this is that entry
-__device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, uint32_t rvo, uint32_t rvl, MGScan& m,
-                         uint32_t (&kw)[16], uint32_t (&sw)[16]) {
-  const uint8_t* base = r.base;
-  const uint32_t mlen = r.len;
-  if (vl < 272) return false;
-  uint32_t h[4], rh[4] = {0u, 0u, 0u, 0u};
-  window16(base, mlen, vo, h);
-  if (MOCHI_W2_REFCMP && rvo != ~0u && rvl >= 8) window16(base, mlen, rvo, rh);  // beside this value's header
-  const RefHead ref = MOCHI_W2_REFCMP && rvo != ~0u ? ref_head(rh, rvo, rvl) : RefHead{~0u, 0, 0, 0, 0, false};
-  const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
-  uint32_t n1, L1, et, kl;
-  if (c1 < 0x80u) {
-    n1 = 1;
-    L1 = c1;
-    et = c2;
-    kl = wbyte(h, 3);
-  } else if (c2 < 0x80u) {
-    n1 = 2;
-    L1 = (c1 & 0x7Fu) | (c2 << 7);
-    et = wbyte(h, 3);
-    kl = wbyte(h, 4);
-  } else {
-    return false;
-  }
-  if (wbyte(h, 0) != 0x0Au || et != 0x0Au || kl > 60) return false;
-  const uint32_t e1 = vo + 1 + n1, s_tag = e1 + L1, end = vo + vl;
-  const uint32_t p5 = end - 264 - kl;  // the signature entry's tag (its key: kl bytes, as the grant's)
-  if (L1 < kl + 3 + 1 + 8 || s_tag + 2 > p5 || p5 - s_tag - 2 > 60) return false;
-  const uint32_t sl = p5 - s_tag - 2;
-  const uint32_t rest = L1 - 3 - kl;  // gl + its varint
-  if (rest == 129) return false;     // gl = 127 in two bytes: not minimal
-  const uint32_t n2 = rest <= 128 ? 1u : 2u, gl = rest - n2;
-  const uint32_t gpos = e1 + 2 + kl, g0 = gpos + 1 + n2;
-  if (gl > 192) return false;
-  // ---- independent loads: framing words, key / serverId windows, the grant ----
-  const uint32_t gh = ld4(base, gpos), t5 = ld4(base, p5), sh = ld4(base, end - 259);
-  const bool cmp = ref.ok && ref.len == gl;  // the first grant's header word is checked below
-  const uint32_t rgh = cmp ? ld4(base, ref.gpos) : 0u;
-  uint32_t(&k1)[16] = kw;
-  uint32_t k4[16];
-  window64(base, mlen, e1, k1);      // 0x0A kl key
-  window64(base, mlen, p5 + 3, k4);  // 0x0A kl key (the signature entry's)
-  window64(base, mlen, s_tag, sw);   // 0x22 sl serverId
-  const uint32_t L5 = 261 + kl;
-  bool ok = (gh & 0xFFu) == 0x12u &&
-            (n2 == 1 ? ((gh >> 8) & 0xFFu) == gl : ((gh >> 8) & 0xFFFFu) == (((gl & 0x7Fu) | 0x80u) | ((gl >> 7) << 8))) &&
-            t5 == (0x2Au | (((L5 & 0x7Fu) | 0x80u) << 8) | ((L5 >> 7) << 16) | (0x0Au << 24)) &&
-            (sh & 0xFFFFFFu) == 0x028012u && (sw[0] & 0xFFFFu) == (0x22u | (sl << 8));
-  uint32_t kdiff = 0, hi = 0;
-#pragma unroll
-  for (int t = 0; t < 16; t++) {
-    kdiff |= (k1[t] ^ k4[t]) & span_mask(t, 0, 2 + (int)kl);
-    hi |= k1[t] & span_mask(t, 2, 2 + (int)kl);
-    hi |= sw[t] & span_mask(t, 2, 2 + (int)sl);
-  }
-  ok = ok && kdiff == 0 && (hi & 0x80808080u) == 0;
-  // ---- the grant: its high-bit count, its first window, and the compare with the reference grant ----
-  uint32_t w0[16], hib = 0, gdiff = 0;
-  uint32_t ga = g0, ra = ref.off;
-#if MOCHI_W2_SPLIT  // A/B: the grant's windows only after the key / serverId windows are reduced (fewer registers)
-  asm volatile("" : "+v"(ga), "+v"(ra) : "v"(kdiff | hi));
-#endif
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    if (64u * c < gl) {
-      uint32_t w[16], v[16];
-      window64(base, mlen, ga + 64 * c, w);
-      if (cmp) window64(base, mlen, ra + 64 * c, v);
-#pragma unroll
-      for (int t = 0; t < 16; t++) {
-        const uint32_t mk = span_mask(t, 0, (int)gl - 64 * c);
-        hib += __builtin_popcount(w[t] & mk & 0x80808080u);
-        if (cmp) gdiff |= (w[t] ^ v[t]) & mk;
-        if (c == 0) w0[t] = w[t];
-      }
-    }
-  }
-  if (!ok || !grant_match(base, mlen, g0, gl, w0, hib)) return false;
-  m.nge = m.nse = 1;
-  m.g = Entry{e1 + 2, kl, g0, gl, 1, true, false};
-  m.sg = Entry{p5 + 5, kl, end - 256, 256, 1, false, false};
-  m.sid_off = s_tag + 2;
-  m.sid_len = sl;
-  m.first_nc = false;
-  m.same = cmp && gdiff == 0 && (rgh & ref.mask) == ref.word;
-  m.sig_key = true;
-  return true;
-}
 
 // signer = index of the key whose server id is the MultiGrant's serverId.
 // The ids share their prefix ("server-"): the last word filters the
@@ -1083,6 +920,187 @@ __device__ __forceinline__ uint8_t slot_from_window(ByteReader& r, const W2Msg& 
     }
   }
   return slot;
+}
+
+// ---- the reference encoder's MultiGrant, matched from a few wide loads ------
+// encode_multigrant / protobuf-java (MochiProtocol.proto:117-124 + field 5):
+// one grant, fields in number order, each map entry its key then its value,
+//   0x0A L1 { 0x0A kl key 0x12 gl Grant } 0x22 sl serverId
+//   0x2A L5 { 0x0A kl key 0x12 0x80 0x02 signature[256] }
+// the signature entry under the grant's key, key and serverId ASCII (kl, sl <= 60),
+// L1 and gl one or two varint bytes, and the Grant itself in its common
+// canonical shape 0x0A L objectId 0x10 ts 0x22 H transactionHash (<= 192 bytes,
+// ASCII strings).  Every position follows from the first 16 bytes (the
+// signature entry's from the value's end), so the loads after the first are
+// independent of each other -- three load latencies (header, windows, the
+// grant's timestamp) where the walk (next_fld / ByteReader::at) paid one per
+// field, length and word.  Any difference returns false and valid_mg_scan
+// decides; what this accepts, valid_mg_scan accepts with the same MGScan (one
+// grants and one grantSignatures entry of one key and one value each, the grant
+// parsed and canonical -- parse_grant_t's CANON rules).
+#ifndef MOCHI_W2_MATCH
+#define MOCHI_W2_MATCH 1  // A/B: 0 = every MultiGrant through valid_mg_scan
+#endif
+#ifndef MOCHI_W2_EARLY
+// signer and key slot inside the match, from the key / serverId windows, and
+// the grant's windows loaded only after them: those windows die first, 200 ->
+// 161 VGPRs (3 waves per SIMD instead of 2), wire path -0.8 % (3.845 / 3.862
+// vs 3.890 / 3.883 ms, alternated)
+#define MOCHI_W2_EARLY 1
+#endif
+#ifndef MOCHI_W2_REFCMP
+#define MOCHI_W2_REFCMP 1  // A/B: 0 = the matcher leaves the compare with the first grant to prep (+1.2 %)
+#endif
+
+// The common Grant shape, canonical and valid (ASCII strings), from its own
+// windows: `hib` = bytes with the high bit set over the whole grant, w0 = its
+// first 16 bytes, read from the timestamp's tag on with one more window.
+__device__ __forceinline__ bool grant_match(const uint8_t* base, uint32_t mlen, uint32_t g0, uint32_t gl,
+                                            const uint32_t (&w0)[16], uint32_t hib) {
+  const uint32_t L = wbyte(w0, 1);
+  if (wbyte(w0, 0) != 0x0Au || L == 0 || L >= 0x80u || L + 6 > gl) return false;
+  uint32_t tb[4];
+  window16(base, mlen, g0 + 2 + L, tb);
+  if (wbyte(tb, 0) != 0x10u) return false;
+  // timestamp: 1..9 varint bytes, minimal (nonzero last byte; a one-byte 0 is the default, never written)
+  uint32_t k = 0, last = 0;
+  bool end = false;
+#pragma unroll
+  for (uint32_t i = 1; i <= 9; i++) {
+    const uint32_t c = wbyte(tb, i);
+    if (!end) {
+      k = i;
+      last = c;
+      end = c < 0x80u;
+    }
+  }
+  if (!end || last == 0) return false;
+  uint32_t c1 = 0, c2 = 0, tag = 0;  // the bytes after the timestamp (k + 1 <= 10)
+#pragma unroll
+  for (uint32_t i = 2; i <= 10; i++) {
+    if (i == k + 1) {
+      tag = wbyte(tb, i);
+      c1 = wbyte(tb, i + 1);
+      c2 = wbyte(tb, i + 2);
+    }
+  }
+  if (tag != 0x22u) return false;
+  uint32_t hl, nh;
+  if (c1 < 0x80u) {
+    hl = c1;
+    nh = 1;
+  } else if (c2 < 0x80u && c2 != 0) {
+    hl = (c1 & 0x7Fu) | (c2 << 7);
+    nh = 2;
+  } else {
+    return false;
+  }
+  const uint32_t hp = 2 + L + 1 + k + 1 + nh;
+  return hl != 0 && hp + hl == gl && hib == (k - 1) + (nh - 1);
+}
+
+// kw / sw (out): the windows at the grants entry (0x0A kl key) and at the
+// serverId (0x22 sl serverId), for the signer and key-slot lookups
+// (rvo, rvl): the message's first certificate entry's value (ref_head: the grant
+// the prep hint compares with), ~0 = this is that entry
+__device__ bool mg_match(ByteReader& r, uint32_t vo, uint32_t vl, uint32_t rvo, uint32_t rvl, MGScan& m,
+                         uint32_t (&kw)[16], uint32_t (&sw)[16], const W2Msg& s, uint32_t mi,
+                         const uint8_t* __restrict__ ids, const uint32_t* __restrict__ id_off, uint32_t n_ids,
+                         const IdTab& tab) {
+  const uint8_t* base = r.base;
+  const uint32_t mlen = r.len;
+  if (vl < 272) return false;
+  uint32_t h[4], rh[4] = {0u, 0u, 0u, 0u};
+  window16(base, mlen, vo, h);
+  if (MOCHI_W2_REFCMP && rvo != ~0u && rvl >= 8) window16(base, mlen, rvo, rh);  // beside this value's header
+  const RefHead ref = MOCHI_W2_REFCMP && rvo != ~0u ? ref_head(rh, rvo, rvl) : RefHead{~0u, 0, 0, 0, 0, false};
+  const uint32_t c1 = wbyte(h, 1), c2 = wbyte(h, 2);
+  uint32_t n1, L1, et, kl;
+  if (c1 < 0x80u) {
+    n1 = 1;
+    L1 = c1;
+    et = c2;
+    kl = wbyte(h, 3);
+  } else if (c2 < 0x80u) {
+    n1 = 2;
+    L1 = (c1 & 0x7Fu) | (c2 << 7);
+    et = wbyte(h, 3);
+    kl = wbyte(h, 4);
+  } else {
+    return false;
+  }
+  if (wbyte(h, 0) != 0x0Au || et != 0x0Au || kl > 60) return false;
+  const uint32_t e1 = vo + 1 + n1, s_tag = e1 + L1, end = vo + vl;
+  const uint32_t p5 = end - 264 - kl;  // the signature entry's tag (its key: kl bytes, as the grant's)
+  if (L1 < kl + 3 + 1 + 8 || s_tag + 2 > p5 || p5 - s_tag - 2 > 60) return false;
+  const uint32_t sl = p5 - s_tag - 2;
+  const uint32_t rest = L1 - 3 - kl;  // gl + its varint
+  if (rest == 129) return false;     // gl = 127 in two bytes: not minimal
+  const uint32_t n2 = rest <= 128 ? 1u : 2u, gl = rest - n2;
+  const uint32_t gpos = e1 + 2 + kl, g0 = gpos + 1 + n2;
+  if (gl > 192) return false;
+  // ---- independent loads: framing words, key / serverId windows, the grant ----
+  const uint32_t gh = ld4(base, gpos), t5 = ld4(base, p5), sh = ld4(base, end - 259);
+  const bool cmp = ref.ok && ref.len == gl;  // the first grant's header word is checked below
+  const uint32_t rgh = cmp ? ld4(base, ref.gpos) : 0u;
+  uint32_t(&k1)[16] = kw;
+  uint32_t k4[16];
+  window64(base, mlen, e1, k1);      // 0x0A kl key
+  window64(base, mlen, p5 + 3, k4);  // 0x0A kl key (the signature entry's)
+  window64(base, mlen, s_tag, sw);   // 0x22 sl serverId
+  const uint32_t L5 = 261 + kl;
+  bool ok = (gh & 0xFFu) == 0x12u &&
+            (n2 == 1 ? ((gh >> 8) & 0xFFu) == gl : ((gh >> 8) & 0xFFFFu) == (((gl & 0x7Fu) | 0x80u) | ((gl >> 7) << 8))) &&
+            t5 == (0x2Au | (((L5 & 0x7Fu) | 0x80u) << 8) | ((L5 >> 7) << 16) | (0x0Au << 24)) &&
+            (sh & 0xFFFFFFu) == 0x028012u && (sw[0] & 0xFFFFu) == (0x22u | (sl << 8));
+  uint32_t kdiff = 0, hi = 0;
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    kdiff |= (k1[t] ^ k4[t]) & span_mask(t, 0, 2 + (int)kl);
+    hi |= k1[t] & span_mask(t, 2, 2 + (int)kl);
+    hi |= sw[t] & span_mask(t, 2, 2 + (int)sl);
+  }
+  ok = ok && kdiff == 0 && (hi & 0x80808080u) == 0;
+#if MOCHI_W2_EARLY
+  m.signer = ok ? signer_from_window(r, s_tag + 2, sl, sw, ids, id_off, n_ids, tab) : (uint16_t)0xFFFF;
+  m.slot = ok ? slot_from_window(r, s, mi, e1 + 2, kl, k1) : (uint8_t)0xFF;
+  const uint32_t dep = kdiff | hi | m.signer | m.slot;
+#else
+  const uint32_t dep = kdiff | hi;
+#endif
+  // ---- the grant: its high-bit count, its first window, and the compare with the reference grant ----
+  uint32_t w0[16], hib = 0, gdiff = 0;
+  uint32_t ga = g0, ra = ref.off;
+#if MOCHI_W2_EARLY  // the grant's windows only after the key / serverId ones are used
+  asm volatile("" : "+v"(ga), "+v"(ra) : "v"(dep));
+#else
+  (void)dep;
+#endif
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    if (64u * c < gl) {
+      uint32_t w[16], v[16];
+      window64(base, mlen, ga + 64 * c, w);
+      if (cmp) window64(base, mlen, ra + 64 * c, v);
+#pragma unroll
+      for (int t = 0; t < 16; t++) {
+        const uint32_t mk = span_mask(t, 0, (int)gl - 64 * c);
+        hib += __builtin_popcount(w[t] & mk & 0x80808080u);
+        if (cmp) gdiff |= (w[t] ^ v[t]) & mk;
+        if (c == 0) w0[t] = w[t];
+      }
+    }
+  }
+  if (!ok || !grant_match(base, mlen, g0, gl, w0, hib)) return false;
+  m.nge = m.nse = 1;
+  m.g = Entry{e1 + 2, kl, g0, gl, 1, true, false};
+  m.sg = Entry{p5 + 5, kl, end - 256, 256, 1, false, false};
+  m.sid_off = s_tag + 2;
+  m.sid_len = sl;
+  m.first_nc = false;
+  m.same = cmp && gdiff == 0 && (rgh & ref.mask) == ref.word;
+  m.sig_key = true;
+  return true;
 }
 
 // Certificate entries (compact, in wire order per message): message index,
@@ -1393,7 +1411,7 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
     };
     stp.mark(1);
     uint32_t kw[16], sw[16];
-    const bool fast = MOCHI_W2_MATCH && mg_match(r, vo, vl, rvo, rvl, sc, kw, sw);
+    const bool fast = MOCHI_W2_MATCH && mg_match(r, vo, vl, rvo, rvl, sc, kw, sw, s, m, ids, id_off, n_ids, tab);
     bool valid = fast;
     if (!fast) {
       const RefGrant ref = rvo == ~0u     ? RefGrant{}
@@ -1418,10 +1436,12 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
         } else {
           ng = 1;
           const bool have = sc.nse == 1 && (sc.sig_key || key_eq(r, sc.sg.koff, sc.sg.klen, sc.g.koff, sc.g.klen));
-          const uint16_t signer = fast ? signer_from_window(r, sc.sid_off, sc.sid_len, sw, ids, id_off, n_ids, tab)
+          const uint16_t signer = fast ? (MOCHI_W2_EARLY ? sc.signer
+                                                         : signer_from_window(r, sc.sid_off, sc.sid_len, sw, ids, id_off,
+                                                                              n_ids, tab))
                                        : find_signer(r, sc.sid_off, sc.sid_len, ids, id_off, n_ids, &tab);
           stp.mark(4);
-          const uint8_t slot = fast ? slot_from_window(r, s, m, sc.g.koff, sc.g.klen, kw)
+          const uint8_t slot = fast ? (MOCHI_W2_EARLY ? sc.slot : slot_from_window(r, s, m, sc.g.koff, sc.g.klen, kw))
                                     : find_key_slot_rec(r, s, m, sc.g.koff, sc.g.klen);
           stp.mark(5);
           rec(sc.g.voff, sc.g.vlen, signer, have && sc.sg.vlen == MOCHI_RSA_BYTES ? sc.sg.voff : ~0u, slot);
