@@ -932,9 +932,10 @@ __device__ __forceinline__ uint8_t slot_from_window(ByteReader& r, const W2Msg& 
 // canonical shape 0x0A L objectId 0x10 ts 0x22 H transactionHash (<= 192 bytes,
 // ASCII strings).  Every position follows from the first 16 bytes (the
 // signature entry's from the value's end), so the loads after the first are
-// independent of each other -- three load latencies (header, windows, the
-// grant's timestamp) where the walk (next_fld / ByteReader::at) paid one per
-// field, length and word.  Any difference returns false and valid_mg_scan
+// independent of each other -- a handful of load latencies (header; key,
+// serverId and framing windows; the operation key for the slot; the grant's
+// windows; its timestamp) where the walk (next_fld / ByteReader::at) paid one
+// per field, length and word.  Any difference returns false and valid_mg_scan
 // decides; what this accepts, valid_mg_scan accepts with the same MGScan (one
 // grants and one grantSignatures entry of one key and one value each, the grant
 // parsed and canonical -- parse_grant_t's CANON rules).
