@@ -287,9 +287,13 @@ __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t* __restrict_
 }
 
 // Each block places kScatterPer x 256 grants: ranks within the block come from
-// wave_counted_add, then ONE global cursor add per (block, signer) — 489
-// blocks x R adds at C2 instead of 3,906 x R.
-constexpr uint32_t kScatterPer = 8;
+// wave_counted_add, then ONE global cursor add per (block, signer).  16 per
+// thread (3,902 blocks x R cursor adds at C4): the bucket stage 0.175 -> 0.140
+// ms against 8 per thread (7,804 blocks), 0.147 at 32 (alternated A/B)
+#ifndef MOCHI_SCATTER_PER
+#define MOCHI_SCATTER_PER 16
+#endif
+constexpr uint32_t kScatterPer = MOCHI_SCATTER_PER;
 
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint16_t* __restrict__ signer, uint32_t n, uint32_t n_keys,
                                                         uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm) {
