@@ -501,8 +501,9 @@ __device__ bool incoming_cert_ok(const TallyArgs& a, uint32_t c, uint32_t g_lo, 
 // InMemoryDataStore.java:613-640 then write2apply :576-611 including the
 // read/apply step (:594-599, :521-574).
 #ifndef MOCHI_TALLY_WAVES
-#define MOCHI_TALLY_WAVES 3  // amdgpu_waves_per_eu (0 = the compiler's choice: 181 VGPRs, 2 waves per SIMD; 3 waves:
-                             // tally 0.63 -> 0.56 ms at C4; 4 waves spill, 0.75 ms)
+#define MOCHI_TALLY_WAVES 3  // amdgpu_waves_per_eu: at least 3 (the windowed hash compare needs 122 VGPRs: 4 waves
+                             // per SIMD; capped for 5 / 6 waves it spills 36 / 51 and takes 0.63 / 0.65 ms vs 0.54
+                             // at C4, round 5; with the dword-load compare it needed 181 and 3 waves was best)
 #endif
 #if MOCHI_TALLY_WAVES
 #define MOCHI_TALLY_ATTR __attribute__((amdgpu_waves_per_eu(MOCHI_TALLY_WAVES)))
