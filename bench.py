@@ -90,6 +90,7 @@ def parse_args():
     ap.add_argument("--no-cluster", action="store_true", help="skip the in-process cluster (C1 / C5 proxy) leg")
     ap.add_argument("--no-shard-sizes", action="store_true", help="skip the per-rank shard-size leg (16M/2, /4, /8)")
     ap.add_argument("--shard-sizes", action="store_true", help="run the shard-size leg even with --headline-only")
+    ap.add_argument("--no-separate", action="store_true", help="skip the separate-copies C4 leg")
     return ap.parse_args()
 
 
@@ -195,19 +196,119 @@ def roofline(n_grants, pow_ms, traffic=None):
                            "vs_valu_only_peak": round(cios / PEAK_MAC_PER_S, 4)}}
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_devices():
+    """GPUs this process may use, counted without initialising the GPU
+    (torch.cuda.device_count() does not create a HIP context on this image)."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def self_launch(n, argv, poll_s=0.2, grace_s=10.0):
+    """`python bench.py --gpus N` (N > 1) with no launcher environment: start the
+    N rank processes here, before this process makes any GPU call, exactly as
+    `torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1` would
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT per child), and
+    wait for them.  Rank 0's stdout is this process's stdout (the one JSON
+    line); the other ranks' stdout goes to stderr.  The first rank to fail ends
+    the job: the others are terminated (then killed after `grace_s`) so no rank
+    is left waiting in a collective for a peer that is gone, and its exit code
+    is returned.  Fails fast (exit 2) when fewer than N devices are visible.
+    With MOCHI_BENCH_REHEARSAL set (tests/bench_rehearsal.py: gloo on the CPU,
+    the oracle standing in for the device) no device is needed."""
+    import subprocess
+
+    if not os.environ.get("MOCHI_BENCH_REHEARSAL"):
+        have = visible_devices()
+        if have < n:
+            print(f"bench.py: --gpus {n} but {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    import threading
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=r == 0))
+
+    def relay(f):  # rank 0's JSON line to stdout; library chatter (gloo / RCCL banners) to stderr
+        for line in f:
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+
+    reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    reader.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            break
+        if all(c == 0 for c in codes):
+            reader.join()
+            return 0
+        time.sleep(poll_s)
+    print(f"bench.py: a rank exited with {rc}; stopping the others", file=sys.stderr, flush=True)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    t_end = time.time() + grace_s
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, t_end - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc if rc > 0 else 1
+
+
+def rank_env(gpus):
+    """(world, rank, local_rank) from the launcher's environment."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != gpus:
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}")
+    return world, rank, local_rank
+
+
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    rehearsal = os.environ.get("MOCHI_BENCH_REHEARSAL")
+    if rehearsal:  # CPU rehearsal of the rank plumbing (tests only): no device, gloo, the oracle verifies
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location("bench_rehearsal", rehearsal)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        result = mod.rank_main(args, *rank_env(args.gpus))
+        if result is not None:
+            print(json.dumps(result), flush=True)
+        return
     import numpy as np
     import torch
 
     import mochi_hip as mh
     import workload as W
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    world, rank, local_rank = rank_env(args.gpus)
+    if local_rank >= visible_devices():
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but {visible_devices()} GPU(s) visible")
     cfg = CONFIGS[args.config]
     R, k = args.replication or cfg["R"], args.ops_per_txn
     strict = not args.client_predicate
@@ -313,6 +414,8 @@ def main():
         shard_leg = None
         if world == 1 and (args.shard_sizes or (extras and not args.no_shard_sizes)):
             shard_leg = shard_sizes_leg(args, ver, synth, C_total, R, strict, local_rank, stream, stage_ms[2])
+        separate = separate_copies_leg(args, ver, synth, host, R, strict, local_rank, stream, t_max / args.steps) \
+            if extras and not args.no_separate else None
         head = W.head_certs(synth, min(C, 1_000_000 // (R * k) * 4)) if extras else None  # ~4M grants
         hostp = host_path(ver, head.batch, R, strict) if extras else None
         wire_s = W.head_certs(synth, min(C, 250_000)) if extras and not args.no_wire else None
@@ -360,18 +463,21 @@ def main():
                                  "launched beside k_rsa_pow (its blocks run in pow's tail; serialised before "
                                  "it with MOCHI_PREP_SERIAL=1): its span ends after pow's; "
                                  "outside_serial_stages = step - bucket - pow - final - tally"},
-            "prep_dedup": prep_dedup(batch) if rank == 0 else None,
+            "cpu_baseline": cpu,
+            # the side legs in full; the compact `summary` below comes LAST so a tail of the line carries it
             "c3": c3,
             "shard_sizes": shard_leg,
+            "c4_separate_copies": separate,
             "host_path_pcie_inclusive_grants_per_s": hostp["pinned_grants_per_s"] if hostp else None,
             "host_path": hostp,
             "write2_wire_path": wire,
             "producer_signing": signing,
             "cluster_c5_proxy": cluster,
-            "correct_vs_ground_truth": all_ok,
-            "cpu_baseline": cpu,
             "wall_s": round(wall_max, 4),
+            "correct_vs_ground_truth": all_ok,
+            "prep_dedup": prep_dedup(batch) if rank == 0 else None,
         }
+        result["summary"] = summary(result, stage_ms, t_max / args.steps * 1e3)
     if dist is not None:
         # the gathered bitmap is the whole batch's: rank 0 checks it holds its own shard's verdicts
         if rank == 0 and result is not None:
@@ -385,6 +491,88 @@ def main():
     if getattr(args, "native_child", None) is not None and args.native_child.poll() is None:
         args.native_child.kill()  # the wire leg never wrote its input
     ver.close()
+
+
+def summary(res, stage_ms, step_ms):
+    """The figures a reader checks first, compact, as the line's last key: the
+    headline's stage split and roofline fractions, the grant-prep dedup, the C3
+    fractions, the per-rank shard sizes and the separate-copies C4 step."""
+    def g(d, *path):
+        for k in path:
+            if not isinstance(d, dict) or k not in d:
+                return None
+            d = d[k]
+        return d
+
+    out = {"value": res["value"], "ms_per_step": res["ms_per_step"],
+           "stage_ms": {k: round(v, 4) for k, v in zip(("prep_sha256", "bucket", "rsa_pow", "rsa_final", "tally"),
+                                                      stage_ms)},
+           "outside_serial_stages_ms": round(step_ms - sum(stage_ms[1:]), 4),
+           "roofline_frac": g(res, "roofline", "frac"), "roofline_frac_implemented": g(res, "roofline", "implemented",
+                                                                                          "frac"),
+           "prep_dedup": {k: g(res, "prep_dedup", k) for k in ("grants", "prepped", "ratio")},
+           "correct_vs_ground_truth": res["correct_vs_ground_truth"]}
+    if res.get("c3"):
+        out["c3"] = {k: {"grants_per_s": g(res, "c3", k, "grants_per_s"), "frac": g(res, "c3", k, "roofline", "frac")}
+                     for k in ("server_gt", "client_ge")}
+    if res.get("shard_sizes"):
+        out["shard_sizes"] = [{"world": r["world"], "grants_per_s": r["grants_per_s"],
+                               "pow_per_grant_vs_full": r["pow_per_grant_vs_full"], "frac": r["roofline_frac"]}
+                              for r in res["shard_sizes"]["rows"]]
+    sep = res.get("c4_separate_copies")
+    if sep:
+        out["c4_separate_copies"] = {k: sep.get(k) for k in ("grants_per_s", "ms_per_step", "vs_shared_layout",
+                                                             "verdicts_equal_shared_layout", "flags_equal_ground_truth")}
+        out["c4_separate_copies"]["stage_ms"] = sep.get("stage_ms")
+    wire = res.get("write2_wire_path")
+    if wire:
+        out["write2_wire_grants_per_s"] = wire.get("grants_per_s")
+        nat = g(wire, "batcher_native", "rows") or []
+        out["batcher_native"] = [{"mode": r.get("mode"), "threads": r.get("threads"), "contexts": r.get("contexts"),
+                                  "requests_per_s": r.get("requests_per_s"), "p50_us": g(r, "latency_us", "p50"),
+                                  "mismatches": r.get("verdict_mismatches")} for r in nat]
+    if res.get("cpu_baseline"):
+        out["cpu_baseline_grants_per_s"] = g(res, "cpu_baseline", "value")
+    return out
+
+
+def separate_copies_leg(args, ver, synth, head_host, R, strict, dev, stream, head_step_s):
+    """C4 with every grant its own copy of its bytes at a mixed alignment
+    (workload.separate_copies: the layout of grant slices of received
+    Write2ToServer messages -- each replica builds its own Grant,
+    InMemoryDataStore.java:131-140, and the client ships all R MultiGrants,
+    MochiDBClient.java:333-338), timed exactly like the headline.  Grant prep
+    then finds a slot's equal grants by comparing bytes (no shared offsets).
+    Its verdicts and per-op outputs must equal the headline's."""
+    import numpy as np
+
+    import mochi_hip as mh
+    import workload as W
+
+    t0 = time.perf_counter()
+    sc = W.separate_copies(synth)
+    build_s = time.perf_counter() - t0
+    d = mh.DeviceBatch(sc.batch, dev)
+    o = mh.DeviceVerdicts(d.n_grants, d.n_certs, dev, full=True, n_ops=d.n_ops)
+    ver.set_profiling(True)
+    ev_s, _ = timed_steps(lambda: ver.verify_device(d, o, R, strict, stream=stream.cuda_stream), args.steps,
+                          args.warmup, stream)
+    ver.set_profiling(False)
+    prof = ver.read_profile()
+    h = o.to_host()
+    same = all(np.array_equal(getattr(h, k), getattr(head_host, k)) for k in
+               ("grant_flags", "grant_ts", "cert_accept_bits", "cert_reason", "cert_fail_op", "op_decision", "op_g0",
+                "op_ts"))
+    n = sc.batch.n_grants
+    step_s = ev_s / args.steps
+    del d, o
+    return {"grants_per_s": round(n * args.steps / ev_s, 1), "ms_per_step": round(step_s * 1e3, 4),
+            "vs_shared_layout": round(head_step_s / step_s, 4),
+            "stage_ms": {k: round(prof[k], 4) for k in ver.STAGES},
+            "verdicts_equal_shared_layout": bool(same),
+            "flags_equal_ground_truth": bool(np.array_equal(h.grant_flags, synth.expected_flags)),
+            "blob_bytes": int(sc.batch.grant_bytes.nbytes), "layout_build_s": round(build_s, 2),
+            "note": "every grant its own copy after 0-15 filler bytes; vs_shared_layout = headline step / this step"}
 
 
 def c3_leg(args, dev, stream):

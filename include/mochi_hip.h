@@ -223,9 +223,10 @@ int mochi_device_count(void);
  */
 mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_keys, uint32_t key_bytes,
                             uint32_t public_exponent);
-/* Waits for every batcher built on the context to be freed first (a batcher
- * destroyed from its own callback is freed by its last flusher thread a little
- * later), so it must not be called from a callback of such a batcher. */
+/* Never blocks.  With no batcher holding the context it is freed now; while a
+ * batcher built on it is alive (or a batcher destroyed from its own callback is
+ * not yet freed by its last flusher) the context is freed by that batcher's
+ * release instead.  Either way the handle must not be used after the call. */
 void mochi_ctx_destroy(mochi_ctx* ctx);
 
 /*
@@ -581,8 +582,10 @@ int mochi_batcher_stats(mochi_batcher* b, uint64_t* batches, uint64_t* msgs);
  * MOCHI_EINVAL, requests already queued still complete, and the last flusher
  * frees the batcher; the handle must not be used after the call either way.
  * The batcher holds its contexts until it is freed: mochi_ctx_destroy on one of
- * them returns only after that, so a caller that tears down right after its
- * last callback cannot free a context the flusher still uses.  A process that
+ * them while a batcher still holds it returns at once and the context is freed
+ * by the batcher's release (never while a flusher still uses it), so a caller
+ * that tears down right after its last callback -- or closes the context before
+ * the batcher -- neither blocks nor frees a context in use.  A process that
  * exits without destroying the contexts must not exit from a callback. */
 void mochi_batcher_destroy(mochi_batcher* b);
 
@@ -677,6 +680,16 @@ mochi_comm* mochi_comm_init(const uint8_t* id /* [128] */, int n_ranks, int rank
 int mochi_comm_allgather_bits(mochi_comm* c, const uint32_t* d_send, uint32_t words_per_rank, uint32_t* d_recv,
                               void* stream);
 void mochi_comm_destroy(mochi_comm* c);
+
+/* Test hook (host only, no GPU): the per-device protocol mochi_mverify_* use
+ * around the all-gather (multi.cpp run_gather), with n simulated devices whose
+ * device selection / slot fill / collective enqueue fail per bit of the masks
+ * and whose collective is a host rendezvous of all n.  Returns the protocol's
+ * status; *entered_collective = devices that enqueued, *timed_out = devices that
+ * waited `timeout_ms` for a peer that never came (the hang the protocol must
+ * rule out: always 0). */
+int mochi_test_gather_protocol(uint32_t n, uint32_t fail_select, uint32_t fail_fill, uint32_t fail_enqueue,
+                               uint32_t timeout_ms, uint32_t* entered_collective, uint32_t* timed_out);
 
 #ifdef __cplusplus
 }

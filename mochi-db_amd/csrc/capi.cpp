@@ -250,13 +250,14 @@ int set_error(int code, const std::string& msg) {
 }  // namespace mochi
 
 struct mochi_ctx {
-  // batchers built on this context (mochi_batcher_create*): mochi_ctx_destroy
-  // waits until the last of them is freed -- a batcher destroyed from its own
-  // callback is freed later by its last flusher thread, which still uses the
-  // context's streams and pinned buffers until then
+  // batchers built on this context (mochi_batcher_create*) hold it until they
+  // are freed -- a batcher destroyed from its own callback is freed later by
+  // its last flusher thread, which still uses the context's streams and pinned
+  // buffers until then.  mochi_ctx_destroy with a holder left never blocks: it
+  // marks the context and the last holder's release frees it.
   std::mutex ref_mu;
-  std::condition_variable ref_cv;
   int batcher_refs = 0;
+  bool destroy_pending = false;
   int device = 0;
   hipStream_t stream = nullptr;
   uint32_t n_keys = 0;
@@ -309,12 +310,16 @@ void ctx_hold(mochi_ctx* c) {
   std::lock_guard<std::mutex> lk(c->ref_mu);
   c->batcher_refs++;
 }
+void ctx_free(mochi_ctx* c);
+// Nothing touches c after the unlock unless this release is the one that frees
+// it (refs reached 0 with a destroy pending: no other thread may still use c).
 void ctx_release(mochi_ctx* c) {
+  bool free_now;
   {
     std::lock_guard<std::mutex> lk(c->ref_mu);
-    c->batcher_refs--;
+    free_now = --c->batcher_refs == 0 && c->destroy_pending;
   }
-  c->ref_cv.notify_all();
+  if (free_now) ctx_free(c);
 }
 
 // the generation of the last context call made by this thread (multi.cpp reads it
@@ -432,10 +437,20 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
 
 void mochi_ctx_destroy(mochi_ctx* c) {
   if (!c) return;
-  {  // a batcher on this context still alive (e.g. its deferred teardown not yet done)
-    std::unique_lock<std::mutex> lk(c->ref_mu);
-    c->ref_cv.wait(lk, [&] { return c->batcher_refs == 0; });
+  {  // a batcher on this context still alive (its deferred teardown not yet done, or
+     // the caller closed the context before the batcher): the last release frees it
+    std::lock_guard<std::mutex> lk(c->ref_mu);
+    if (c->batcher_refs > 0) {
+      c->destroy_pending = true;
+      return;
+    }
   }
+  mochi::ctx_free(c);
+}
+
+}  // extern "C"
+
+void mochi::ctx_free(mochi_ctx* c) {
   int save = 0;
   (void)hipGetDevice(&save);
   (void)hipSetDevice(c->device);
@@ -459,8 +474,6 @@ void mochi_ctx_destroy(mochi_ctx* c) {
   delete c;
   (void)hipSetDevice(save);
 }
-
-}  // extern "C"
 
 namespace {
 

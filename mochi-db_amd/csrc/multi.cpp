@@ -19,7 +19,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -163,6 +168,7 @@ struct mochi_mctx {
   std::vector<uint32_t*> gathered;  // per device: n_dev * words_per_shard words (device memory)
   std::vector<size_t> gathered_cap;
   uint32_t last_words = 0;
+  bool comm_aborted = false;  // a gather aborted the communicators: rebuilt by the next gather
 };
 
 mochi_mctx* mochi_mctx_create(uint64_t device_mask, const uint8_t* moduli_be, uint32_t n_keys, uint32_t key_bytes,
@@ -298,56 +304,113 @@ void slice_batch(const mochi_batch* B, uint32_t c0, uint32_t c1, SubBatch& s) {
   }
 }
 
-// The all-gather step.  Each device's shard verdicts are already on that
-// device: the accept bitmap of the context call that just returned (a slice of
-// its output buffer).  Per device (one thread each) it is copied device to
-// device into the device's slot of its gather buffer (zero-padded to W words),
-// then one ncclAllGather fills every device's buffer, and bits_out comes from
-// ONE device-to-host copy of device 0's.  A context whose device bitmap is not
-// the final verdict (messages decided by the host fallback decoder) uploads its
-// host bits into its slot instead.
+// The all-gather protocol, one host thread per device (multi.cpp's gather_bits
+// and the CPU test hook mochi_test_gather_protocol drive the same code):
+//   1. select the device (once: every later step runs on this thread) and make
+//      its gather buffer;
+//   -- barrier: a failure in 1 on ANY device is seen by all of them here, and
+//      then no device enters the collective (no peer is left waiting in it);
+//   2. fill the device's slot; a local failure is recorded, and the device still
+//      enqueues its part of the collective so its peers complete;
+//   3. enqueue the collective;
+//   -- barrier: if ANY device failed to enqueue, every device aborts its
+//      communicator (which ends the peers' pending collective kernels) instead
+//      of waiting on its stream; the communicators are rebuilt on the next call;
+//   4. wait for the device's stream.
+// Returns the first error of any device, after every thread has joined.
+struct GatherOps {
+  std::function<int(int)> select, prep, fill, enqueue, finish, abort;
+};
+
+class Barrier {
+ public:
+  explicit Barrier(int n) : n_(n) {}
+  void arrive_and_wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const uint64_t gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      gen_++;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, count_ = 0;
+  uint64_t gen_ = 0;
+};
+
+int run_gather(int n, const GatherOps& ops, std::string* what) {
+  std::vector<int> rc_setup(n, MOCHI_OK), rc_fill(n, MOCHI_OK), rc_enq(n, MOCHI_OK), rc_fin(n, MOCHI_OK);
+  Barrier bar(n);
+  std::atomic<bool> setup_failed{false}, enq_failed{false};
+  auto dev = [&](int i) {
+    int r = ops.select(i);
+    if (r == MOCHI_OK) r = ops.prep(i);
+    rc_setup[i] = r;
+    if (r) setup_failed = true;
+    bar.arrive_and_wait();
+    if (setup_failed) return;
+    rc_fill[i] = ops.fill(i);
+    rc_enq[i] = ops.enqueue(i);
+    if (rc_enq[i]) enq_failed = true;
+    bar.arrive_and_wait();
+    if (enq_failed) {
+      ops.abort(i);
+      return;
+    }
+    rc_fin[i] = ops.finish(i);
+  };
+  std::vector<std::thread> th;
+  for (int i = 0; i < n; i++) th.emplace_back(dev, i);
+  for (auto& t : th) t.join();
+  const std::vector<int>* stages[4] = {&rc_setup, &rc_fill, &rc_enq, &rc_fin};
+  const char* names[4] = {"device selection / gather buffer", "slot fill", "all-gather enqueue (communicators aborted)",
+                          "all-gather completion"};
+  for (int s = 0; s < 4; s++)
+    for (int i = 0; i < n; i++)
+      if ((*stages[s])[i]) {
+        if (what) *what = std::string(names[s]) + " failed on device slot " + std::to_string(i);
+        return (*stages[s])[i];
+      }
+  return MOCHI_OK;
+}
+
+// Each device's shard verdicts are already on that device: the accept bitmap
+// of the context call that just returned (a slice of its output buffer).  Per
+// device it is copied device to device into the device's slot of its gather
+// buffer (zero-padded to W words), then one ncclAllGather fills every device's
+// buffer, and bits_out comes from ONE device-to-host copy of device 0's.  A
+// context whose device bitmap is not the final verdict (messages decided by the
+// host fallback decoder) uploads its host bits into its slot instead.
 int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::vector<std::vector<uint32_t>>& shard_bits,
                 const std::vector<uint64_t>& gen, uint32_t* bits_out) {
   const int n = (int)m->devices.size();
   const uint32_t W = mochi_shard_words((uint32_t)n, cert_lo.data());
-  std::vector<int> rc(n, MOCHI_OK);
-  // Phase 1 (no collective): every device's gather buffer.  A failure here is
-  // seen by all threads after the join, before any of them enters the
-  // collective, so no device is left waiting in ncclAllGather for a peer that
-  // bailed out.
-  auto prep = [&](int i) {
-    if (hipSetDevice(m->devices[i]) != hipSuccess) {
-      rc[i] = MOCHI_EHIP;
-      return;
-    }
-    const size_t bytes = 4 * (size_t)W * n;
-    if (bytes > m->gathered_cap[i]) {
-      if (m->gathered[i]) (void)hipFree(m->gathered[i]);
-      m->gathered[i] = nullptr;
-      m->gathered_cap[i] = 0;
-      if (hipMalloc(&m->gathered[i], bytes) != hipSuccess) {
-        rc[i] = MOCHI_ENOMEM;
-        return;
-      }
-      m->gathered_cap[i] = bytes;
-    }
-  };
-  {
-    std::vector<std::thread> th;
-    for (int i = 0; i < n; i++) th.emplace_back(prep, i);
-    for (auto& t : th) t.join();
+  if (m->comm_aborted) {  // a previous call aborted the communicators: rebuild them
+    for (auto& c : m->comm)
+      if (c) (void)ncclCommDestroy(c), c = nullptr;
+    const ncclResult_t r = ncclCommInitAll(m->comm.data(), n, m->devices.data());
+    if (r != ncclSuccess) return mfail(MOCHI_EHIP, std::string("ncclCommInitAll (rebuild): ") + nccl_str(r));
+    m->comm_aborted = false;
   }
-  for (int r : rc)
-    if (r) return mfail(r, "bitmap all-gather buffers failed");
-  // Phase 2: fill the slot and all-gather.  A local failure filling the slot
-  // (memset, device copy, upload) is recorded, but the device still takes part
-  // in the collective so its peers complete; the error is reported after every
-  // thread has joined.
-  auto work = [&](int i) {
-    if (hipSetDevice(m->devices[i]) != hipSuccess) {
-      rc[i] = MOCHI_EHIP;  // cannot reach the device's stream at all
-      return;
-    }
+  GatherOps ops;
+  ops.select = [&](int i) { return hipSetDevice(m->devices[i]) == hipSuccess ? MOCHI_OK : MOCHI_EHIP; };
+  ops.prep = [&](int i) {
+    const size_t bytes = 4 * (size_t)W * n;
+    if (bytes <= m->gathered_cap[i]) return MOCHI_OK;
+    if (m->gathered[i]) (void)hipFree(m->gathered[i]);
+    m->gathered[i] = nullptr;
+    m->gathered_cap[i] = 0;
+    if (hipMalloc(&m->gathered[i], bytes) != hipSuccess) return MOCHI_ENOMEM;
+    m->gathered_cap[i] = bytes;
+    return MOCHI_OK;
+  };
+  ops.fill = [&](int i) {
     uint32_t* slot = m->gathered[i] + (size_t)W * i;
     const uint32_t need = words(cert_lo[i + 1] - cert_lo[i]);  // <= W
     hipError_t e = hipMemsetAsync(slot, 0, 4 * (size_t)W, m->stream[i]);
@@ -362,20 +425,30 @@ int gather_bits(mochi_mctx* m, const std::vector<uint32_t>& cert_lo, const std::
         e = hipMemcpyAsync(slot, shard_bits[i].data(), 4 * have, hipMemcpyHostToDevice, m->stream[i]);
       }
     }
-    if (e != hipSuccess) rc[i] = MOCHI_EHIP;
-    if (ncclAllGather(slot, m->gathered[i], W, ncclUint32, m->comm[i], m->stream[i]) != ncclSuccess ||
-        hipStreamSynchronize(m->stream[i]) != hipSuccess)
-      rc[i] = MOCHI_EHIP;
+    return e == hipSuccess ? MOCHI_OK : MOCHI_EHIP;
   };
-  std::vector<std::thread> th;
-  for (int i = 0; i < n; i++) th.emplace_back(work, i);
-  for (auto& t : th) t.join();
-  for (int r : rc)
-    if (r) return mfail(r, "bitmap all-gather failed");
-  m->last_words = W;
-  std::vector<uint32_t> all((size_t)W * n);
+  ops.enqueue = [&](int i) {
+    uint32_t* slot = m->gathered[i] + (size_t)W * i;
+    return ncclAllGather(slot, m->gathered[i], W, ncclUint32, m->comm[i], m->stream[i]) == ncclSuccess ? MOCHI_OK
+                                                                                                       : MOCHI_EHIP;
+  };
+  ops.finish = [&](int i) { return hipStreamSynchronize(m->stream[i]) == hipSuccess ? MOCHI_OK : MOCHI_EHIP; };
+  std::atomic<bool> aborted{false};
+  ops.abort = [&](int i) {
+    (void)ncclCommAbort(m->comm[i]);
+    m->comm[i] = nullptr;
+    aborted = true;
+    return MOCHI_OK;
+  };
   int save = 0;
   (void)hipGetDevice(&save);
+  std::string what;
+  const int rc = run_gather(n, ops, &what);
+  if (aborted) m->comm_aborted = true;
+  (void)hipSetDevice(save);
+  if (rc) return mfail(rc, "bitmap all-gather: " + what);
+  m->last_words = W;
+  std::vector<uint32_t> all((size_t)W * n);
   (void)hipSetDevice(m->devices[0]);
   const hipError_t e = hipMemcpy(all.data(), m->gathered[0], 4 * all.size(), hipMemcpyDeviceToHost);
   (void)hipSetDevice(save);
@@ -485,6 +558,50 @@ int mochi_mctx_gathered_bits(mochi_mctx* m, int i, const uint32_t** d_bits, uint
   *d_bits = m->gathered[i];
   if (words_per_device) *words_per_device = m->last_words;
   return MOCHI_OK;
+}
+
+// CPU test hook for the all-gather protocol (run_gather): n device threads with
+// no GPU, the collective a host rendezvous that only completes when all n
+// threads enqueued (or one aborted); a thread that never arrives makes the
+// others time out after `timeout_ms` -- the hang the protocol must prevent.
+int mochi_test_gather_protocol(uint32_t n, uint32_t fail_select, uint32_t fail_fill, uint32_t fail_enqueue,
+                               uint32_t timeout_ms, uint32_t* entered_collective, uint32_t* timed_out) {
+  if (n == 0 || n > 32) return MOCHI_EINVAL;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint32_t arrived = 0, timeouts = 0;
+  bool aborted = false;
+  GatherOps ops;
+  ops.select = [&](int i) { return (fail_select >> i) & 1 ? MOCHI_EHIP : MOCHI_OK; };
+  ops.prep = [&](int) { return MOCHI_OK; };
+  ops.fill = [&](int i) { return (fail_fill >> i) & 1 ? MOCHI_EHIP : MOCHI_OK; };
+  ops.enqueue = [&](int i) {
+    if ((fail_enqueue >> i) & 1) return MOCHI_EHIP;
+    std::lock_guard<std::mutex> lk(mu);
+    arrived++;
+    cv.notify_all();
+    return MOCHI_OK;
+  };
+  ops.finish = [&](int) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (!cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return arrived == n || aborted; })) {
+      timeouts++;
+      return MOCHI_EHIP;
+    }
+    return aborted ? MOCHI_EHIP : MOCHI_OK;
+  };
+  ops.abort = [&](int) {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+    return MOCHI_OK;
+  };
+  std::string what;
+  const int rc = run_gather((int)n, ops, &what);
+  if (entered_collective) *entered_collective = arrived;
+  if (timed_out) *timed_out = timeouts;
+  if (rc) mfail(rc, what);
+  return rc;
 }
 
 }  // extern "C"

@@ -215,6 +215,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.mochi_comm_allgather_bits.argtypes = [vp, vp, u32, vp, vp]
     lib.mochi_comm_destroy.argtypes = [vp]
+    lib.mochi_test_gather_protocol.argtypes = [u32, u32, u32, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
     lib.mochi_host_alloc.restype = vp
     lib.mochi_host_alloc.argtypes = [ctypes.c_uint64]
     lib.mochi_host_free.argtypes = [vp]
@@ -1080,7 +1081,8 @@ class Batcher:
         library defers the teardown (queued requests still complete; its last
         flusher frees it); the handle is dropped here either way, so a later
         close() / __del__ cannot free the batcher a second time.  The library
-        holds the contexts until the batcher is freed (mochi_ctx_destroy waits)."""
+        holds the contexts until the batcher is freed (a mochi_ctx_destroy before that
+        returns at once and the batcher's release frees the context)."""
         h, self.h = self.h, None
         if h:
             self.lib.mochi_batcher_destroy(h)

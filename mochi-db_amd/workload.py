@@ -559,6 +559,35 @@ def make_batch_unique(R: int, n_certs: int, k: int = 1, first_cert: int = 0, see
     return Synth(batch, np.zeros(C, np.int64), fault, rf, flags)
 
 
+def separate_copies(s: Synth, seed: int = SEED, chunk: int = 1 << 18) -> Synth:
+    """The same certificates with every grant its OWN copy of its bytes, each
+    after 0..15 bytes of filler (mixed alignments), in (certificate, MultiGrant)
+    order -- the layout of grant slices of received Write2ToServer messages: in
+    the reference every replica builds its own Grant (InMemoryDataStore.java:131-140)
+    and the client ships all R MultiGrants (MochiDBClient.java:333-338).  Same
+    bytes, signatures and ground truth as `s`; only grant_off and the blob differ,
+    so grant prep must find equal grants by comparing bytes (no equal offsets)."""
+    b = s.batch
+    n = b.n_grants
+    ln = np.ascontiguousarray(b.grant_len[:n], np.int64)
+    pad = (_h(seed, 11, np.arange(n, dtype=np.uint64)) % np.uint64(16)).astype(np.int64)
+    start = np.zeros(n + 1, np.int64)
+    np.cumsum(pad + ln, out=start[1:])
+    new_off = start[:-1] + pad
+    out = np.full(int(start[-1]) or 1, 0xEE, np.uint8)
+    src_all = np.ascontiguousarray(b.grant_off[:n], np.int64)
+    W_ = int(ln.max()) if n else 0
+    col = np.arange(W_, dtype=np.int64)[None, :]
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        m = col < ln[lo:hi, None]
+        out[(new_off[lo:hi, None] + col)[m]] = b.grant_bytes[(src_all[lo:hi, None] + col)[m]]
+    nb = Batch(grant_bytes=out, grant_off=new_off.astype(np.uint64), grant_len=b.grant_len[:n].copy(), sig=b.sig,
+               signer=b.signer, grant_key=b.grant_key, cert_grant_off=b.cert_grant_off, cert_op_off=b.cert_op_off,
+               op_key=b.op_key, op_flags=b.op_flags, expected_hash=b.expected_hash)
+    return Synth(nb, s.template, s.fault, s.fault_replica, s.expected_flags)
+
+
 def save_batch(path: str, s: Synth) -> None:
     b = s.batch
     np.savez(path, **{f: getattr(b, f) for f in ("grant_bytes", "grant_off", "grant_len", "sig", "signer",

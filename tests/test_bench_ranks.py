@@ -96,3 +96,79 @@ def test_bench_rank_plumbing_gloo(tmp_path, world, total_grants):
     assert float(z["t_max"]) >= float(z["own"])
     plan = z["plan"]
     assert plan[0] == 0 and plan[-1] == C_total and all(int(p) % 32 == 0 for p in plan[1:-1])
+
+
+def _bench_cmd(world, total_grants, cache, extra=()):
+    return [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+            "--grants-total", str(total_grants), "--cache-dir", cache] + list(extra)
+
+
+def _plain_env(**kv):
+    """A plain shell's environment: no launcher variables at all."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "GROUP_RANK")}
+    env.update(kv)
+    return env
+
+
+@pytest.mark.parametrize("world,total_grants", [(2, 4 * 300), (4, 4 * 333 + 4), (8, 4 * 520)])
+def test_bench_self_launch_gloo(tmp_path, world, total_grants):
+    """`python bench.py --gpus N` with no launcher env starts its own N ranks (bench.self_launch)
+    and rank 0 prints the one JSON line; the gathered bitmap == the single-process oracle."""
+    import json
+    import subprocess
+
+    import mochi_hip as mh
+    import oracle_ffi as O
+    import workload as W
+
+    cache = str(tmp_path / "cache")
+    pool = W.build_pool(R=4, k=1, P=64, P_f=16, cache_dir=cache)  # sign once, ranks load the cache
+    out = str(tmp_path / "r0.npz")
+    env = _plain_env(MOCHI_BENCH_REHEARSAL=os.path.join(ROOT, "tests", "bench_rehearsal.py"),
+                     MOCHI_REHEARSAL_OUT=out, OMP_NUM_THREADS="1")
+    p = subprocess.run(_bench_cmd(world, total_grants, cache), env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout  # only rank 0 prints, one line
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == world and res["correct_vs_ground_truth"] and res["gathered_bitmap_matches_rank0"]
+    z = np.load(out)
+    C_total = int(z["C_total"])
+    full = W.make_batch(pool, C_total)
+    ref = O.verify_batch(pool.moduli, full.batch, 4, True, 2)
+    assert np.array_equal(mh.unpack_bits(z["full"], C_total), ref.cert_accept)
+    assert (~ref.cert_accept).any()
+    assert res["grants_total"] == full.batch.n_grants
+    plan = z["plan"]
+    assert len(plan) == world + 1 and plan[-1] == C_total
+
+
+def test_bench_self_launch_rank_failure_ends_job(tmp_path):
+    """A rank that dies after the rendezvous must not leave its peers waiting in the first
+    barrier: the launcher stops them and exits with the failed rank's code."""
+    import subprocess
+    import time
+
+    cache = str(tmp_path / "cache")
+    import workload as W
+
+    W.build_pool(R=4, k=1, P=64, P_f=16, cache_dir=cache)
+    env = _plain_env(MOCHI_BENCH_REHEARSAL=os.path.join(ROOT, "tests", "bench_rehearsal.py"),
+                     MOCHI_REHEARSAL_FAIL_RANK="1", OMP_NUM_THREADS="1")
+    t0 = time.time()
+    p = subprocess.run(_bench_cmd(3, 4 * 200, cache), env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert time.time() - t0 < 240
+    assert not p.stdout.strip()
+
+
+def test_bench_self_launch_needs_devices(tmp_path):
+    """Without the rehearsal hook, --gpus N with fewer than N visible GPUs fails fast
+    (this container has none) instead of starting ranks."""
+    import subprocess
+
+    p = subprocess.run(_bench_cmd(2, 4 * 100, str(tmp_path)), env=_plain_env(HIP_VISIBLE_DEVICES=""),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2 and "GPU(s) visible" in p.stderr

@@ -159,3 +159,36 @@ def test_write1_classify_reference_semantics():
     # OTHER payloads clear allWriteOk only (:284-287)
     assert mh.write1_classify([[ok(0, [(0, 5, 0)]), (mh.W1_OTHER, 1, [])]])[0] == mh.W1_THROW_REFUSED
 
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_gather_protocol_never_strands_a_peer(n):
+    """The per-device protocol mochi_mverify_* run around the RCCL all-gather
+    (multi.cpp run_gather), on the CPU with simulated devices: a device whose
+    selection fails keeps every device out of the collective; one whose slot fill
+    fails still joins it (its peers complete) and the error is reported; one
+    whose enqueue fails makes every device abort instead of waiting.  No device
+    ever waits for a peer that never comes (timed_out == 0) and every case
+    returns an error, not a hang."""
+    import ctypes
+
+    import mochi_hip as mh
+
+    lib = mh.load_library()
+    entered, timed_out = ctypes.c_uint32(), ctypes.c_uint32()
+
+    def run(sel=0, fill=0, enq=0):
+        rc = lib.mochi_test_gather_protocol(n, sel, fill, enq, 5000, ctypes.byref(entered), ctypes.byref(timed_out))
+        return rc, entered.value, timed_out.value
+
+    assert run() == (mh.OK, n, 0)
+    rc, e, t = run(sel=1 << 1)
+    assert rc != mh.OK and e == 0 and t == 0
+    rc, e, t = run(sel=1 << (n - 1) | 1)
+    assert rc != mh.OK and e == 0 and t == 0
+    rc, e, t = run(fill=1 << 1)
+    assert rc != mh.OK and e == n and t == 0
+    assert "slot fill" in lib.mochi_last_error().decode()
+    rc, e, t = run(enq=1 << (n - 1))
+    assert rc != mh.OK and e == n - 1 and t == 0
+    assert "enqueue" in lib.mochi_last_error().decode()

@@ -284,6 +284,26 @@ def test_c4_16m_batch_bit_exact():
     for lo in np.linspace(head, b.n_grants - 1000, 8).astype(np.int64):
         of, ot = O.verify_grants(moduli_for(R), b, int(lo), int(lo) + 1000, 8)
         np.testing.assert_array_equal(g.grant_flags[lo:lo + 1000], of[lo:lo + 1000])
+    # The launch bench.py times: the whole 16M-grant batch resident in HBM, ONE
+    # mochi_verify_batch_device call (7,800+ dynamic pow groups, the LDS-staged
+    # certificate prep at 4M certificates), in the bench's layout (one copy of a
+    # certificate's grant bytes) and with every grant its own copy at a mixed
+    # alignment (wire slices: prep must compare bytes).  Every certificate's
+    # verdict, reason, failing op and per-op outputs == the oracle tally above.
+    import torch
+
+    for name, sb in (("shared", s), ("separate", W.separate_copies(s))):
+        dev = mh.DeviceBatch(sb.batch, 0)
+        out = mh.DeviceVerdicts(dev.n_grants, dev.n_certs, 0, full=True, n_ops=dev.n_ops)
+        for _ in range(2):  # twice: the second call reuses the context's scratch as the bench's steps do
+            ver.verify_device(dev, out, R, True, stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        h = out.to_host()
+        np.testing.assert_array_equal(h.grant_flags, s.expected_flags, err_msg=name)
+        np.testing.assert_array_equal(h.grant_ts, g.grant_ts, err_msg=name)
+        np.testing.assert_array_equal(h.grant_valid_bits, g.grant_valid_bits, err_msg=name)
+        assert_same_certs(h, o)
+        del dev, out
     ver.close()
 
 

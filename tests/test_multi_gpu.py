@@ -152,3 +152,4 @@ def _d2h(dev_ptr, words):
     out = np.zeros(words, np.uint32)
     assert hip.hipMemcpy(out.ctypes.data, dev_ptr, 4 * words, 2) == 0  # hipMemcpyDeviceToHost
     return out
+

@@ -30,3 +30,27 @@ def test_txn_hashes():
     h = W._txn_hashes(np.array([0, 5, 123456789], np.uint64))
     assert h[1].tobytes().decode() == hashlib.sha512(b"txn-5").hexdigest()
     assert h[2].tobytes().decode() == W.txn_hash_hex(123456789)
+
+
+def test_separate_copies_layout(tmp_path):
+    """workload.separate_copies: every grant its own copy at a mixed alignment, the same
+    bytes per grant, and the oracle's verdicts unchanged (the C4 separate-copy leg)."""
+    import numpy as np
+
+    import oracle_ffi as O
+    import workload as W
+
+    pool = W.build_pool(R=4, k=2, P=64, P_f=16, cache_dir=str(tmp_path))
+    s = W.make_batch(pool, 700, first_cert=5)
+    t = W.separate_copies(s)
+    b, c = s.batch, t.batch
+    for i in range(b.n_grants):
+        x = b.grant_bytes[int(b.grant_off[i]):int(b.grant_off[i]) + int(b.grant_len[i])]
+        y = c.grant_bytes[int(c.grant_off[i]):int(c.grant_off[i]) + int(c.grant_len[i])]
+        assert np.array_equal(x, y)
+    assert len(np.unique(c.grant_off)) == c.n_grants  # no two grants share a copy
+    assert len(set((c.grant_off % 16).tolist())) == 16  # every alignment occurs
+    v1 = O.verify_batch(pool.moduli, b, 4, True, 4)
+    v2 = O.verify_batch(pool.moduli, c, 4, True, 4)
+    for k in ("grant_flags", "grant_ts", "cert_accept_bits", "cert_reason", "cert_fail_op"):
+        assert np.array_equal(getattr(v1, k), getattr(v2, k)), k

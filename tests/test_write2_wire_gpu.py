@@ -691,3 +691,26 @@ def test_wire_layout_matcher_edges(pool4):
     for k in ("sig_under_other_key", "sig_255", "key_bad_utf8", "grant_200_bytes"):
         assert not acc[k].any(), k
     ver.close()
+
+
+def test_context_closed_before_its_batcher(pool4):
+    """Closing a Verifier while a Batcher on it is alive (explicit close, or __del__
+    order in a host language) neither blocks nor frees the context under the
+    batcher: mochi_ctx_destroy returns at once, the batcher keeps verifying with
+    the oracle's verdicts, and the batcher's own teardown frees the context."""
+    import time
+
+    ver = _ver(pool4)
+    s = W.make_batch(pool4, 64, first_cert=9900)
+    wb = W.encode_wire_batch(s)
+    ids, off = W.server_id_table(4)
+    ref, _ = O.verify_write2(pool4.moduli, ids, off, wb, 4, True)
+    b = mh.Batcher(ver, 4, True, max_msgs=64, max_wait_us=100)
+    t0 = time.perf_counter()
+    ver.close()
+    assert time.perf_counter() - t0 < 5.0
+    for i in range(wb.n_msgs):
+        msg = wb.wire[int(wb.msg_off[i]):int(wb.msg_off[i]) + int(wb.msg_len[i])].tobytes()
+        acc, reason, _, _ = b.verify(msg, wb.expected_hash[i].tobytes())
+        assert acc == bool(ref.cert_accept[i]) and reason == ref.cert_reason[i]
+    b.close()
