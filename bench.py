@@ -91,6 +91,8 @@ def parse_args():
     ap.add_argument("--no-shard-sizes", action="store_true", help="skip the per-rank shard-size leg (16M/2, /4, /8)")
     ap.add_argument("--shard-sizes", action="store_true", help="run the shard-size leg even with --headline-only")
     ap.add_argument("--no-separate", action="store_true", help="skip the separate-copies C4 leg")
+    ap.add_argument("--layout", choices=("shared", "separate"), default="shared",
+                    help="headline grant-byte layout (separate: workload.separate_copies; profiling runs)")
     return ap.parse_args()
 
 
@@ -346,6 +348,8 @@ def main():
     # SURVEY §8d stream, unique grant bytes per certificate, signed on this GPU (k_rsa_sign)
     t_gen = time.perf_counter()
     synth = W.make_batch_unique(R, C, k, first_cert=c_lo, device=local_rank)
+    if args.layout == "separate":
+        synth = W.separate_copies(synth)
     gen_s = time.perf_counter() - t_gen
     moduli = [mh.pem_modulus(p) for p in W.load_keys(R)]
     if cpu_child is not None:

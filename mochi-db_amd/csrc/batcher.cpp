@@ -80,6 +80,10 @@ struct Flusher {
   std::vector<uint8_t> status, reason, fail_op, op_dec;
   std::vector<uint32_t> accept, op_g0;
   std::vector<int64_t> op_ts;
+  // when this flusher's last batch completed (under the batcher's mu, before its
+  // callers were woken): the queue length then and the batch's size
+  size_t q_at_done = 0, last_n = 0;
+  std::chrono::steady_clock::time_point t_done;
 };
 
 // the batcher whose flusher runs on this thread (a callback re-entering the
@@ -100,6 +104,7 @@ struct mochi_batcher {
   uint32_t live = 0;             // flusher threads still in run()
   uint32_t waiters = 0;          // blocking callers not yet out of their wait (mu is theirs until then)
   uint64_t n_batches = 0, n_msgs = 0;
+  uint32_t collecting = 0;  // flushers waiting for the callers their last batch released (take())
   std::vector<Flusher> fl;
 
   // Frees the flushers' pinned buffers, then lets the contexts go: however the
@@ -112,18 +117,31 @@ struct mochi_batcher {
     for (mochi_ctx* c : cs) mochi::ctx_release(c);
   }
 
-  // Takes the next batch: waits for work, then for a full batch or for the
-  // oldest pending request's deadline (re-evaluated whenever a sibling flusher
-  // took the queue's head).  Returns false when stopped and drained.
-  bool take(std::vector<Request*>& batch) {
+  // Takes the next batch.  Waits for work; then, if this flusher has just
+  // completed a batch, until the callers that batch released are back (the
+  // queue holds what it held at completion plus that batch's size) or
+  // max_wait_us after the completion: blocking callers resubmit within
+  // microseconds of their verdicts, and taking the first of them alone would
+  // split them into alternating batches that each wait for the other's flight
+  // (2 blocking workers on one context: every request paid two GPU round
+  // trips).  An idle flusher takes what is queued at once; a full batch
+  // (max_msgs) is taken at once.  Returns false when stopped and drained.
+  bool take(Flusher& f, std::vector<Request*>& batch) {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      cv_work.wait(lk, [&] { return stop || !q.empty(); });
+      // an idle flusher leaves the queue to a sibling that is collecting its callers
+      cv_work.wait(lk, [&] { return stop || (!q.empty() && (f.last_n || collecting == 0 || q.size() >= max_msgs)); });
       if (q.empty()) return false;  // stopped and drained
-      while (!stop && !q.empty() && q.size() < max_msgs) {
-        const auto deadline = q.front()->t_enq + std::chrono::microseconds(max_wait_us);
-        if (std::chrono::steady_clock::now() >= deadline) break;
-        cv_work.wait_until(lk, deadline);
+      if (f.last_n) {
+        const size_t want = f.q_at_done + f.last_n < max_msgs ? f.q_at_done + f.last_n : max_msgs;
+        const auto deadline = f.t_done + std::chrono::microseconds(max_wait_us);
+        collecting++;
+        while (!stop && !q.empty() && q.size() < want) {
+          if (std::chrono::steady_clock::now() >= deadline) break;
+          cv_work.wait_until(lk, deadline);
+        }
+        collecting--;
+        f.last_n = 0;
       }
       if (q.empty()) continue;  // a sibling flusher took it: never verify M = 0
       const size_t n = q.size() < max_msgs ? q.size() : max_msgs;
@@ -137,7 +155,7 @@ struct mochi_batcher {
   void run(Flusher& f) {
     t_flushing = this;
     std::vector<Request*> batch, owned;
-    while (take(batch)) {
+    while (take(f, batch)) {
       verify(f, batch);  // fills the blocking callers' slots, runs the submitters' callbacks
       // the submitted (heap) requests are freed here; a blocking caller's request
       // lives on its stack and may be gone the moment it sees `done`, so it is
@@ -151,6 +169,9 @@ struct mochi_batcher {
           if (!r->cb) r->done = true;
         n_batches++;
         n_msgs += batch.size();
+        f.q_at_done = q.size();
+        f.last_n = batch.size();
+        f.t_done = std::chrono::steady_clock::now();
       }
       cv_done.notify_all();
       for (Request* r : owned) delete r;
@@ -269,8 +290,10 @@ struct mochi_batcher {
 
   void enqueue(Request* r) {  // mu held
     q.push_back(r);
-    if (q.size() == 1) cv_work.notify_one();
-    else if (q.size() >= max_msgs) cv_work.notify_all();  // whichever flusher is idle takes it
+    // every waiting flusher re-checks: a collecting one counts the arrival, an idle
+    // one takes the queue unless a sibling is collecting (notify_one could wake
+    // an idle flusher that then waits on, and the collector would sleep to its deadline)
+    cv_work.notify_all();
   }
 };
 

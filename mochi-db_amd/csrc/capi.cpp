@@ -265,7 +265,7 @@ struct mochi_ctx {
   mochi::FoldKey* d_fold = nullptr;  // per-key k_rsa_pow fold matrices (~101 KB each)
   std::mutex mu;
   // verify scratch
-  DevBuf digest, ts, hash_off, hash_len, flags, count, cursor, total, perm, xbuf, dedup;
+  DevBuf digest, ts, hash_off, hash_len, flags, count, cursor, total, perm, xbuf, dedup, lead;
   // host-path device copies
   DevBuf dev_in, dev_out;
   PinnedBuf pin_in, pin_out;
@@ -541,19 +541,16 @@ hipError_t scratch_release(mochi_ctx* c, hipStream_t st) {
   return hipEventRecord(c->ev_scratch, st);
 }
 
+int ensure_scratch(mochi_ctx* c, uint32_t N, uint32_t C);
+
 int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o, hipStream_t st,
                const uint32_t* op_out_off = nullptr, const uint32_t* grant_same = nullptr) {
   const uint32_t N = b->n_grants, C = b->n_certs;
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
   if (slots > 0xFFFFFFF0ull) return fail(MOCHI_EINVAL, "batch too large");
   int rc;
-  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure((size_t)N)) ||
-      (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
-      (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
-      (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
-      (rc = c->total.ensure(mochi::kTotalWords * sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
-      (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots)))
-    return rc;
+  if ((uint64_t)N + C > 0xFFFFFFF0ull) return fail(MOCHI_EINVAL, "batch too large");
+  if ((rc = ensure_scratch(c, N, C))) return rc;
   mochi::LaunchArgs a;
   memset(&a, 0, sizeof a);
   a.n_grants = N;
@@ -582,7 +579,9 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.strict_gt = p->strict_gt ? 1 : 0;
   a.keys = c->d_keys;
   a.fold = c->d_fold;
-  a.digest = c->digest.as<uint32_t>();
+  a.digest = c->digest.as<uint32_t>();  // distinct prep results: N + C entries (kernels.h)
+  a.n_dist = N + C;
+  a.lead = c->lead.as<uint32_t>();
   a.ts = o->grant_ts ? o->grant_ts : c->ts.as<int64_t>();
   a.hash_off = c->hash_off.as<uint64_t>();
   a.hash_len = c->hash_len.as<uint32_t>();
@@ -658,12 +657,16 @@ void par_memcpy(void* dst, const void* src, size_t n) {
   for (auto& x : th) x.join();
 }
 
-int ensure_scratch(mochi_ctx* c, uint32_t N) {
+// Verify scratch for N grants of C certificates: per grant (ts, flags, rare,
+// lead), per distinct prep result (N + C: digest, hash slice), per slot (perm, z).
+int ensure_scratch(mochi_ctx* c, uint32_t N, uint32_t C) {
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
+  const size_t ND = (size_t)N + C;
   int rc;
-  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * (size_t)N)) || (rc = c->dedup.ensure((size_t)N)) ||
-      (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * (size_t)N)) ||
-      (rc = c->hash_len.ensure(sizeof(uint32_t) * (size_t)N)) || (rc = c->flags.ensure((size_t)N)) ||
+  if ((rc = c->digest.ensure(sizeof(uint32_t) * 8 * ND)) || (rc = c->dedup.ensure((size_t)N)) ||
+      (rc = c->ts.ensure(sizeof(int64_t) * (size_t)N)) || (rc = c->hash_off.ensure(sizeof(uint64_t) * ND)) ||
+      (rc = c->hash_len.ensure(sizeof(uint32_t) * ND)) || (rc = c->flags.ensure((size_t)N)) ||
+      (rc = c->lead.ensure(sizeof(uint32_t) * (size_t)N)) ||
       (rc = c->count.ensure(sizeof(uint32_t) * c->n_keys)) || (rc = c->cursor.ensure(sizeof(uint32_t) * c->n_keys)) ||
       (rc = c->total.ensure(mochi::kTotalWords * sizeof(uint32_t))) || (rc = c->perm.ensure(sizeof(uint32_t) * (size_t)slots)) ||
       (rc = c->xbuf.ensure(sizeof(uint32_t) * mochi::kL * (size_t)slots)))
@@ -690,7 +693,7 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
     size_t seg[kNumSeg];
   };
   std::vector<Chunk> ch;
-  uint32_t max_grants = 0;
+  uint32_t max_grants = 0, max_certs = 0;
   for (uint32_t c0 = 0; c0 < C || (C == 0 && ch.empty());) {
     uint32_t c1 = c0;
     do c1 = c1 + 32 < C ? c1 + 32 : C;
@@ -720,6 +723,7 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
     k.lo = lo;
     k.hi = hi;
     if (k.g1 - k.g0 > max_grants) max_grants = k.g1 - k.g0;
+    if (k.c1 - k.c0 > max_certs) max_certs = k.c1 - k.c0;
     ch.push_back(k);
     if (C == 0) break;
     c0 = c1;
@@ -782,7 +786,7 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
                o_g0 = take(o->op_g0 ? sizeof(uint32_t) * O : 0), o_ots = take(o->op_ts ? sizeof(int64_t) * O : 0);
   int rc;
   if ((rc = c->pin_in.ensure(in_total)) || (rc = c->dev_in.ensure(in_total)) || (rc = c->pin_out.ensure(out_total)) ||
-      (rc = c->dev_out.ensure(out_total)) || (rc = ensure_scratch(c, max_grants)))
+      (rc = c->dev_out.ensure(out_total)) || (rc = ensure_scratch(c, max_grants, max_certs)))
     return rc;
   while (c->chunk_ev.size() < 2 * nchunks) {
     hipEvent_t e;
@@ -976,9 +980,10 @@ int w2_verify(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, 
     return rc;
   if (!decode_only) {  // the verify scratch grows only once the stream has drained
     const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
-    if (sizeof(uint32_t) * mochi::kL * slots > c->xbuf.cap || sizeof(uint32_t) * 8 * (size_t)N > c->digest.cap)
+    if (sizeof(uint32_t) * mochi::kL * slots > c->xbuf.cap || sizeof(uint32_t) * 8 * ((size_t)N + a.M) > c->digest.cap ||
+        sizeof(uint32_t) * (size_t)N > c->lead.cap)
       HIP_TRY(hipStreamSynchronize(st));
-    if ((rc = ensure_scratch(c, N))) return rc;
+    if ((rc = ensure_scratch(c, N, a.M))) return rc;
   }
   a.N = N;
   a.sig_src = c->w2_sigsrc.as<uint64_t>();

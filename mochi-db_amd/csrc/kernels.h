@@ -33,10 +33,12 @@ struct LaunchArgs {
   const KeyEntry* keys;
   const FoldKey* fold;  // per-key fold matrices (k_rsa_pow)
   // scratch (context-owned)
-  uint32_t* digest;    // [8][N]
-  int64_t* ts;         // [N]
-  uint64_t* hash_off;  // [N]
-  uint32_t* hash_len;  // [N]
+  uint32_t* digest;    // [8][n_dist]  distinct results (prep_dev.h PrepArgs)
+  int64_t* ts;         // [N]  (may be the caller's grant_ts output)
+  uint64_t* hash_off;  // [n_dist]
+  uint32_t* hash_len;  // [n_dist]
+  uint32_t* lead;      // [N] distinct index per grant (with dedup; null: none)
+  uint32_t n_dist;     // stride of the distinct arrays: >= N + C with dedup (0 = N)
   uint8_t* flags;      // [N]  (may be the caller's grant_flags output)
   uint32_t* count;     // [n_keys]
   uint32_t* cursor;    // [n_keys]
@@ -91,7 +93,7 @@ hipError_t launch_rsa_sign(const uint8_t* blob, const uint64_t* goff, const uint
 hipError_t launch_withhold(const uint8_t* flags, uint32_t n, uint8_t* sig, uint32_t* rejected, hipStream_t stream);
 hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t stream);
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream);
-void launch_rsa_final(const LaunchArgs& a, hipStream_t stream);
+void launch_rsa_final(const LaunchArgs& a, const uint32_t* lead, uint32_t n_dist, hipStream_t stream);
 void launch_rsa_raw(const LaunchArgs& a, hipStream_t stream);  // dbg_y path (mochi_rsa_public_op)
 
 }  // namespace mochi

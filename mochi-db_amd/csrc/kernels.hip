@@ -47,11 +47,17 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep(const PrepAr
 // builds the Grant from the same objectId, transaction hash and timestamp,
 // InMemoryDataStore.java:131-140), and PrepOut is a function of the bytes.
 // k_grant_prep_cert (lane = certificate) preps the first grant of each key slot
-// (up to two slots) and stores its results for every later grant of the slot
-// with the same bytes -- compared as bytes (equal offsets suffice; wire-path
-// grants are separate copies, which the decoder may already have matched:
-// `same`), never assumed.  The rest (a grant that differs from its slot's
-// first, a third slot) keeps its flag (memset 1) and k_grant_prep_rare preps it.
+// (up to two slots) and hands its result to every later grant of the slot with
+// the same bytes -- compared as bytes (equal offsets suffice; wire-path grants
+// are separate copies, which the decoder may already have matched: `same`),
+// never assumed.  The rest (a grant that differs from its slot's first, a third
+// slot) keeps its flag (memset 1) and k_grant_prep_rare preps it.
+//
+// Results are stored once per DISTINCT grant (prep_dev.h PrepArgs): the first
+// slot's digest and hash slice at index c (consecutive lanes, consecutive
+// words: coalesced, and k_rsa_final's lanes -- consecutive certificates of one
+// signer -- read them coalesced too), a second slot's at d_base + g; every
+// grant gets only its own timestamp, flags and lead index (13 bytes, not 53).
 // ---------------------------------------------------------------------------
 struct PrepCertArgs {
   const uint8_t* grant_key;
@@ -61,12 +67,12 @@ struct PrepCertArgs {
   uint8_t* rare;         // [N]: 1 = prepped by k_grant_prep_rare (preset to 1: a grant outside every certificate too)
 };
 
-// The block's first-slot results go out through LDS: each lane puts its
-// leader's results in `lo` and marks the leader and its byte-equal grants in
-// `ref`; then the block stores them grant by grant (consecutive lanes,
-// consecutive grants), not lane = certificate at a 4-grant stride (PMC: 2.58 GB
-// written for 0.86 GB of results that way).  A block whose certificates hold
-// more than kPrepBlockGrants grants, and second slots, store directly.
+// The block's first-slot per-grant outputs go out through LDS: each lane puts
+// its leader's timestamp and flags in `lo` and marks the leader and its
+// byte-equal grants in `ref`; then the block stores them grant by grant
+// (consecutive lanes, consecutive grants), not lane = certificate at a 4-grant
+// stride.  A block whose certificates hold more than kPrepBlockGrants grants,
+// and second slots, store directly.
 constexpr uint32_t kPrepBlockGrants = 2048;
 #ifndef MOCHI_SAME_HINT_CHECK
 #define MOCHI_SAME_HINT_CHECK 0
@@ -75,10 +81,21 @@ constexpr uint32_t kPrepBlockGrants = 2048;
 #define MOCHI_PREP_LDS_STORE 1  // A/B
 #endif
 
-struct PrepOutLds {  // PrepOut in 13 words
-  uint32_t h[8];
-  uint32_t ts_lo, ts_hi, hash_rel, hash_len, flags;
+struct PrepOutLds {  // a leader's per-grant outputs and its byte offset
+  uint32_t ts_lo, ts_hi, flags;
+  uint32_t goff_lo, goff_hi;
 };
+
+// Byte compares of separate copies (a slot's later grants whose offsets differ
+// from its first grant's and that the decoder did not match) are not done by
+// the certificate's lane: there each compare is one more dependent memory round
+// trip per follower (C4 with separate copies: +1.5 ms).  The staged pass marks
+// them (rare = 2) with their results stored optimistically and the leader's
+// byte offset parked in hash_off[d_base + h] (the follower's own distinct slot,
+// unused unless the bytes differ), and k_grant_match compares them 16 lanes per
+// grant, coalesced; a mismatch becomes rare = 1 (prepped on its own).
+constexpr uint32_t kMatchMaxLen = 256;  // 16 lanes x 16 bytes; longer grants compare in the certificate's lane
+constexpr uint16_t kRefMatch = 0x8000u;
 
 __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const PrepArgs a, const PrepCertArgs p) {
 #if MOCHI_PREP_LDS_STORE
@@ -93,7 +110,7 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const P
   __syncthreads();
 #else
   const bool staged = false;
-  const uint32_t G0 = 0;
+  const uint32_t G0 = 0, c0 = 0;
   uint16_t* ref = nullptr;
   PrepOutLds* lo = nullptr;
 #endif
@@ -120,41 +137,45 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const P
       }
       if (!first) continue;  // decided in its slot's first grant's pass
       if (leaders++ == 2) break;  // a third slot: its grants are left to k_grant_prep_rare (rare stays 1)
-      // g leads its slot: prep it, then hand its results to every later grant of the
-      // slot with the same bytes; a grant that differs stays flagged
+      // g leads its slot: prep it, store its distinct result, then hand it to every
+      // later grant of the slot with the same bytes; a grant that differs stays flagged
       const bool via_lds = staged && leaders == 1;
       PrepOut o;
       const uint64_t og = a.goff[g];
       const uint32_t lg = a.glen[g];
       grant_prep_bytes(a.blob + og, lg, o);
+      const uint32_t d = leaders == 1 ? c : a.d_base + g;
+      grant_prep_store_dist(a, d, og, o);
       if (via_lds) {
         PrepOutLds& e = lo[threadIdx.x];
-#pragma unroll
-        for (int q = 0; q < 8; q++) e.h[q] = o.h[q];
         e.ts_lo = (uint32_t)o.ts;
         e.ts_hi = (uint32_t)((uint64_t)o.ts >> 32);
-        e.hash_rel = o.hash_rel;
-        e.hash_len = o.hash_len;
         e.flags = o.flags;
+        e.goff_lo = (uint32_t)og;
+        e.goff_hi = (uint32_t)(og >> 32);
         ref[g - G0] = (uint16_t)threadIdx.x;
       } else {
-        grant_prep_store(a, g, o);
+        grant_prep_store_grant(a, g, d, o.ts, o.flags);
         p.rare[g] = 0;
       }
 #pragma unroll 1
       for (uint32_t h = g + 1; h < g_hi; h++) {
         if (p.grant_key[h] != s) continue;
+        if (a.glen[h] != lg) continue;
         const uint64_t oh = a.goff[h];
         // the decoder's match (`same`) is taken only with equal lengths as well; with
         // MOCHI_SAME_HINT_CHECK=1 (a CI build) it must also survive the byte compare
-        const bool eq = a.glen[h] == lg &&
-                        ((p.same && p.same[h] == g && (!MOCHI_SAME_HINT_CHECK || bytes_equal(a.blob + oh, a.blob + og, lg))) ||
-                         oh == og || bytes_equal(a.blob + oh, a.blob + og, lg));
-        if (!eq) continue;
+        const bool hinted = p.same && p.same[h] == g && !MOCHI_SAME_HINT_CHECK;
+        const bool known = hinted || oh == og;
+        if (via_lds && !known && lg <= kMatchMaxLen) {  // compared by k_grant_match
+          ref[h - G0] = (uint16_t)threadIdx.x | kRefMatch;
+          continue;
+        }
+        if (!known && !bytes_equal(a.blob + oh, a.blob + og, lg)) continue;
         if (via_lds) {
           ref[h - G0] = (uint16_t)threadIdx.x;
         } else {
-          grant_prep_store(a, h, o);
+          grant_prep_store_grant(a, h, d, o.ts, o.flags);
           p.rare[h] = 0;
         }
       }
@@ -165,21 +186,119 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const P
   if (staged) {
 #pragma unroll 1
     for (uint32_t i = threadIdx.x; i < G1 - G0; i += blockDim.x) {
-      const uint32_t r = ref[i];
-      if (r == 0xFFFFu) continue;  // a rare grant, or a second slot's (stored directly)
+      const uint32_t rr = ref[i];
+      if (rr == 0xFFFFu) continue;  // a rare grant, or a second slot's (stored directly)
+      const uint32_t r = rr & 0xFFu;
       const PrepOutLds& e = lo[r];
-      PrepOut o;
-#pragma unroll
-      for (int q = 0; q < 8; q++) o.h[q] = e.h[q];
-      o.ts = (int64_t)(((uint64_t)e.ts_hi << 32) | e.ts_lo);
-      o.hash_rel = e.hash_rel;
-      o.hash_len = e.hash_len;
-      o.flags = (uint8_t)e.flags;
-      grant_prep_store(a, G0 + i, o);
-      p.rare[G0 + i] = 0;
+      grant_prep_store_grant(a, G0 + i, c0 + r, (int64_t)(((uint64_t)e.ts_hi << 32) | e.ts_lo), (uint8_t)e.flags);
+      if (rr & kRefMatch) {  // optimistic: k_grant_match compares the bytes with the leader's
+        a.hash_off[(size_t)a.d_base + G0 + i] = ((uint64_t)e.goff_hi << 32) | e.goff_lo;
+        p.rare[G0 + i] = 2;
+      } else {
+        p.rare[G0 + i] = 0;
+      }
     }
   }
 #endif
+}
+
+// Separate copies marked by k_grant_prep_cert (rare == 2): 16 lanes per grant,
+// lane j compares bytes [16j, 16j + 16) of the grant with its slot leader's
+// (offset parked in hash_off[d_base + h]).  A wave takes 256 grants at a time:
+// one coalesced load of their flags (a dword per lane), and spans without a
+// candidate (every one when a certificate's grants share their bytes) are
+// skipped; otherwise each lane stages its four grants' length and offsets in
+// LDS (coalesced loads), and the wave compares 4 grants per group over the 64
+// four-grant groups that hold a candidate, kMatchUnroll groups at a time with
+// their window loads issued together -- one memory round trip per
+// kMatchUnroll groups.  Equal: rare = 0 (the leader's results stored by
+// prep_cert stand); different: rare = 1.
+constexpr uint32_t kMatchUnroll = 4;
+
+struct MatchMeta {
+  uint64_t off, lead_off;
+  uint32_t len, pad;
+};
+
+__global__ __launch_bounds__(256) void k_grant_match(const PrepArgs a, uint8_t* __restrict__ rare) {
+  __shared__ MatchMeta meta[4][256];
+  const uint32_t lane = threadIdx.x & 63, sub = lane >> 4, piece = lane & 15, wv = threadIdx.x >> 6;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+  MatchMeta* m = meta[wv];
+#pragma unroll 1
+  for (uint64_t base = (uint64_t)wave * 256; base < a.n; base += (uint64_t)n_waves * 256) {
+    const uint64_t g4 = base + 4 * lane;  // this lane's four flags
+    uint32_t f = 0;
+    if (g4 + 4 <= a.n) {
+      f = *(const uint32_t*)(rare + g4);  // rare is 256-byte aligned, base and 4 * lane multiples of 4
+    } else {
+      for (uint32_t b = 0; b < 4; b++)
+        if (g4 + b < a.n) f |= (uint32_t)rare[g4 + b] << (8 * b);
+    }
+    uint64_t todo = __ballot((f & 0x02020202u) != 0);  // flags are 0, 1 or 2
+    if (!todo) continue;
+    if (f & 0x02020202u) {  // stage the metadata of this lane's candidates
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++)
+        if (((f >> (8 * b)) & 0xFFu) == 2) {
+          const uint64_t h = g4 + b;
+          MatchMeta& e = m[4 * lane + b];
+          e.off = a.goff[h];
+          e.lead_off = a.hash_off[(size_t)a.d_base + h];
+          e.len = a.glen[h];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll 1
+    while (todo) {
+      uint32_t q[kMatchUnroll];
+#pragma unroll
+      for (uint32_t u = 0; u < kMatchUnroll; u++) {
+        q[u] = todo ? (uint32_t)__builtin_ctzll(todo) : 64u;
+        if (todo) todo &= todo - 1;
+      }
+      bool cand[kMatchUnroll], diff[kMatchUnroll];
+#pragma unroll
+      for (uint32_t u = 0; u < kMatchUnroll; u++) {
+        const uint32_t fq = q[u] < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)f, (int)q[u]) : 0u;
+        cand[u] = ((fq >> (8 * sub)) & 0xFFu) == 2;
+        diff[u] = false;
+      }
+      // all kMatchUnroll groups' window loads before any compare: no branch between
+      // them (lanes without a byte to compare read a dummy line of `rare`)
+      uint32_t x[kMatchUnroll][4], y[kMatchUnroll][4], len[kMatchUnroll];
+      const uint32_t pos = 16 * piece;
+#pragma unroll
+      for (uint32_t u = 0; u < kMatchUnroll; u++) {
+        const MatchMeta& e = m[4 * (q[u] & 63) + sub];
+        len[u] = cand[u] ? e.len : 0u;
+        const bool valid = pos < len[u];
+        const uintptr_t ax = valid ? (uintptr_t)(a.blob + e.off + pos) : (uintptr_t)rare;
+        const uintptr_t ay = valid ? (uintptr_t)(a.blob + e.lead_off + pos) : (uintptr_t)rare;
+        const uint32_t shx = (uint32_t)(ax & 15), shy = (uint32_t)(ay & 15);
+        window16_nb(ax, valid && shx != 0 && pos - shx + 16 < len[u], x[u]);
+        window16_nb(ay, valid && shy != 0 && pos - shy + 16 < len[u], y[u]);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kMatchUnroll; u++) {
+        uint32_t d = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const int32_t left = (int32_t)(len[u] - pos) - 4 * t;  // len <= pos: every mask 0
+          const uint32_t mk = left >= 4 ? ~0u : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
+          d |= (x[u][t] ^ y[u][t]) & mk;
+        }
+        diff[u] = d != 0;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kMatchUnroll; u++) {
+        const uint64_t dm = __ballot(diff[u]);
+        if (cand[u] && piece == 0) rare[base + 4 * q[u] + sub] = ((dm >> (16 * sub)) & 0xFFFFull) ? 1 : 0;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next span's staging overwrites m
+  }
 }
 
 // The flagged grants, compacted per block: each block scans kRareSpan flags
@@ -387,8 +506,9 @@ struct TallyArgs {
   const uint8_t* blob;
   const uint64_t* grant_off;
   const uint32_t* grant_len;
-  const uint64_t* hash_off;
+  const uint64_t* hash_off;  // distinct results, index lead[g] (g without lead)
   const uint32_t* hash_len;
+  const uint32_t* lead;
   const uint8_t* expected;
   uint32_t n_certs, majority, strict_gt, quorum_mode;
   uint32_t* accept_bits;
@@ -573,7 +693,8 @@ __global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs 
         uint32_t why = MOCHI_ACCEPT;
         if (first == 0xFFFFFFFFu) why = MOCHI_REJECT_NO_GRANT;                                      // :588
         else if (!(a.strict_gt ? cnt > a.majority : cnt >= a.majority)) why = MOCHI_REJECT_BELOW_QUORUM;  // :590
-        else if (!hash_matches(a.blob, a.hash_off[first], a.hash_len[first], expected))
+        else if (!hash_matches(a.blob, a.hash_off[a.lead ? a.lead[first] : first],
+                               a.hash_len[a.lead ? a.lead[first] : first], expected))
           why = MOCHI_REJECT_HASH_MISMATCH;                                                       // :591,605-607
         else if (!(fl & MOCHI_OP_HAS_SVOC)) why = MOCHI_REJECT_NO_SVOC;                           // :592-593
         else {
@@ -697,7 +818,13 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   // per SIMD-half, nothing to hide its latency) it cost the step 5-9 ms
   // (DESIGN.md section 9).  The fork comes after bucketing: beside prep, the
   // short bucket kernels (which gate k_rsa_pow) took ~4x longer.
-  const PrepArgs pa{a.blob, a.grant_off, a.grant_len, N, a.digest, a.ts, a.hash_off, a.hash_len, a.flags};
+  // grant dedup (k_grant_prep_cert + k_grant_prep_rare): results stored once per distinct
+  // grant, read through `lead`; without it every grant is its own distinct index
+  const bool dedup = a.rare && a.lead && a.cert_grant_off && C && !dedup_off();
+  const uint32_t nd = a.n_dist ? a.n_dist : N;
+  const PrepArgs pa{a.blob,     a.grant_off, a.grant_len, N,        nd,      dedup ? C : 0u,
+                    a.digest,   a.ts,        a.hash_off,  a.hash_len, a.flags, dedup ? a.lead : nullptr};
+  const uint32_t* lead = dedup ? a.lead : nullptr;
   const bool prep = N && !a.skip_prep_tally;
   const bool fork = prep && a.aux;
   hipStream_t ps = fork ? a.aux : st;
@@ -721,11 +848,13 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   auto grant_prep = [&](hipStream_t ps) -> hipError_t {
     mark(kStagePrep, false, ps);
     if (prep) {
-      if (a.rare && a.cert_grant_off && C && !dedup_off()) {
+      if (dedup) {
         const PrepCertArgs pc{a.grant_key, a.cert_grant_off, a.grant_same, C, a.rare};
         hipError_t e = hipMemsetAsync(a.rare, 1, N, ps);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_grant_prep_cert, dim3(cdiv(C, 256)), dim3(256), 0, ps, pa, pc);
+        const uint32_t mblocks = cdiv(N, 4 * 256) < 2048 ? cdiv(N, 4 * 256) : 2048;  // 4 waves x 256 grants
+        hipLaunchKernelGGL(k_grant_match, dim3(mblocks), dim3(256), 0, ps, pa, a.rare);
         hipLaunchKernelGGL(k_grant_prep_rare, dim3(cdiv(N, kRareSpan)), dim3(256), 0, ps, pa, (const uint8_t*)a.rare);
       } else {
         hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
@@ -771,7 +900,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   }
   mark(kStageFinal, false, st);
   if (N) {
-    launch_rsa_final(a, st);
+    launch_rsa_final(a, lead, nd, st);
     if (a.grant_valid_bits)
       hipLaunchKernelGGL(k_pack_bits, dim3(cdiv(N, 256)), dim3(256), 0, st, a.flags, N, (uint8_t)MOCHI_GRANT_SIG_OK,
                          a.grant_valid_bits);
@@ -798,6 +927,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     t.grant_len = a.grant_len;
     t.hash_off = a.hash_off;
     t.hash_len = a.hash_len;
+    t.lead = lead;
     t.expected = a.expected_hash;
     t.n_certs = C;
     t.majority = a.majority;

@@ -9,16 +9,25 @@
 
 namespace mochi {
 
+// Per grant: its timestamp and parse flags (outputs of the call) and, with
+// grant dedup, `lead` = the index of its DISTINCT result -- the digest and the
+// transactionHash slice, stored once per distinct grant (k_rsa_final and
+// k_tally read them through lead).  Distinct index d: certificate c's first key
+// slot -> c; any other grant prepped on its own -> d_base + g (d_base = the
+// number of certificates; 0 and no lead array without dedup: d = g).
 struct PrepArgs {
   const uint8_t* blob;
   const uint64_t* goff;
   const uint32_t* glen;
   uint32_t n;           // grants to prep (0 = none)
-  uint32_t* digest;     // [8][n]
-  int64_t* ts;          // [n]
-  uint64_t* hash_off;   // [n]
-  uint32_t* hash_len;   // [n]
-  uint8_t* flags;       // [n]
+  uint32_t nd;          // stride of the distinct arrays (>= d_base + n)
+  uint32_t d_base;
+  uint32_t* digest;     // [8][nd]   distinct
+  int64_t* ts;          // [n]       per grant
+  uint64_t* hash_off;   // [nd]      distinct
+  uint32_t* hash_len;   // [nd]      distinct
+  uint8_t* flags;       // [n]       per grant
+  uint32_t* lead;       // [n] per grant, or null (d = g)
 };
 
 // What the prep of one grant's bytes yields; a pure function of the bytes, so
@@ -42,6 +51,27 @@ __device__ __forceinline__ void window16(const uint8_t* p, uint32_t l, uint32_t 
   const v4u c0 = a16[0];  // holds byte pos (< l)
   v4u c1 = {0u, 0u, 0u, 0u};
   if (sh != 0 && pos - sh + 16 < l) c1 = a16[1];
+  const uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const uint32_t m4 = 0u - ((sh >> 2) & 1u), m8 = 0u - ((sh >> 3) & 1u);
+  uint32_t e1[7], e[5];
+#pragma unroll
+  for (int j = 0; j < 7; j++) e1[j] = (d[j + 1] & m4) | (d[j] & ~m4);
+#pragma unroll
+  for (int j = 0; j < 5; j++) e[j] = (e1[j + 2] & m8) | (e1[j] & ~m8);
+  const uint32_t r = 8 * (sh & 3);
+#pragma unroll
+  for (int t = 0; t < 4; t++) w[t] = __builtin_amdgcn_alignbit(e[t + 1], e[t], r);
+}
+
+// window16 without branches (a batch of them can be issued together): 16 bytes
+// at addr; `two` = the second aligned chunk holds a wanted byte (else the first
+// is loaded twice).  addr must be readable (callers pass a dummy when unused).
+__device__ __forceinline__ void window16_nb(uintptr_t addr, bool two, uint32_t (&w)[4]) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u* a16 = (const v4u*)(addr & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(addr & 15);
+  const v4u c0 = a16[0];
+  const v4u c1 = a16[two ? 1 : 0];
   const uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
   const uint32_t m4 = 0u - ((sh >> 2) & 1u), m8 = 0u - ((sh >> 3) & 1u);
   uint32_t e1[7], e[5];
@@ -132,19 +162,29 @@ __device__ __forceinline__ void grant_prep_bytes(const uint8_t* p, uint32_t l, P
   o.flags = ok ? MOCHI_GRANT_PARSED : 0;
 }
 
-__device__ __forceinline__ void grant_prep_store(const PrepArgs& a, uint32_t i, const PrepOut& o) {
+// The distinct result d of grant bytes at offset `goff` (hash_off is absolute).
+__device__ __forceinline__ void grant_prep_store_dist(const PrepArgs& a, uint32_t d, uint64_t goff, const PrepOut& o) {
 #pragma unroll
-  for (int q = 0; q < 8; q++) a.digest[(size_t)q * a.n + i] = o.h[q];
-  a.ts[i] = o.ts;
-  a.hash_off[i] = a.goff[i] + o.hash_rel;
-  a.hash_len[i] = o.hash_len;
-  a.flags[i] = o.flags;
+  for (int q = 0; q < 8; q++) a.digest[(size_t)q * a.nd + d] = o.h[q];
+  a.hash_off[d] = goff + o.hash_rel;
+  a.hash_len[d] = o.hash_len;
+}
+
+// Grant g's own outputs, its result at distinct index d.
+__device__ __forceinline__ void grant_prep_store_grant(const PrepArgs& a, uint32_t g, uint32_t d, int64_t ts,
+                                                       uint8_t flags) {
+  a.ts[g] = ts;
+  a.flags[g] = flags;
+  if (a.lead) a.lead[g] = d;
 }
 
 __device__ __forceinline__ void grant_prep_one(const PrepArgs& a, uint32_t i) {
   PrepOut o;
-  grant_prep_bytes(a.blob + a.goff[i], a.glen[i], o);
-  grant_prep_store(a, i, o);
+  const uint64_t goff = a.goff[i];
+  grant_prep_bytes(a.blob + goff, a.glen[i], o);
+  const uint32_t d = a.d_base + i;
+  grant_prep_store_dist(a, d, goff, o);
+  grant_prep_store_grant(a, i, d, o.ts, o.flags);
 }
 
 // Bytes [pos, pos + 64) of the `len` bytes at `base` (any alignment) as 16

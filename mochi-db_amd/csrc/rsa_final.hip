@@ -34,21 +34,63 @@
 #define MOCHI_FINAL_DYN 0
 #endif
 
+// MOCHI_FINAL_STAMPS (measurement builds only, `make ab VSRC=rsa_final`): per
+// wave, s_memtime cycles in the operand loads (=2: an explicit vmcnt(0) wait
+// after them, so their latency is separated from the product), the product,
+// the digest load + fold, the final Montgomery step + store, and the whole
+// kernel; read back with mochi_debug_final_stamps() (scripts/final_stamps.py)
+#ifndef MOCHI_FINAL_STAMPS
+#define MOCHI_FINAL_STAMPS 0
+#endif
+
 namespace mochi {
+#if MOCHI_FINAL_STAMPS
+__device__ unsigned long long g_final_stamps[4096][6];
+#endif
 namespace {
 
-// One lane's operands, as loaded: the signature's 16-byte rows and z's limbs.
+struct FStamps {
+  uint64_t load = 0, prod = 0, fold = 0, check = 0, n = 0;
+};
+
+__device__ __forceinline__ uint64_t fstamp() {
+#if MOCHI_FINAL_STAMPS
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
+}
+
+// A/B: an explicit vmcnt(0) wait once a half-group's operands are issued.
+// Phase stamps (scripts/final_stamps.py, round 6) showed the product 3.2k
+// cycles per item faster behind one wait than with the compiler's waits for
+// single limbs interleaved into its first columns.
+#ifndef MOCHI_FINAL_WAIT
+#define MOCHI_FINAL_WAIT 1
+#endif
+
+// One lane's operands, as loaded: the signature's 16-byte rows, z's limbs, and
+// -- issued with them, so their latency hides under the product instead of
+// stalling the fold and the flag store (stamps: ~2k cycles each per item) --
+// the grant's digest (through its distinct-result index) and its parse flags.
 struct FinalOps {
   uint4 sr[16];
   uint32_t z[kL];
-  uint32_t g;
+  uint32_t hw[8];
+  uint32_t g, fl, d;
 };
 
 __device__ __forceinline__ void final_load(uint32_t slot, uint32_t g_lead, const uint32_t* __restrict__ perm,
                                            uint32_t n_slots, const uint8_t* __restrict__ sig,
-                                           const uint32_t* __restrict__ zin, FinalOps& o) {
+                                           const uint32_t* __restrict__ zin, const uint32_t* __restrict__ lead,
+                                           const uint8_t* __restrict__ flags, FinalOps& o) {
   o.g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
   const uint32_t gg = o.g != 0xFFFFFFFFu ? o.g : g_lead;  // inactive lanes shadow the lead grant
+  o.d = lead ? lead[gg] : gg;  // the grant's distinct prep result (kernels.hip); its digest: final_load_digest
+  o.fl = flags[gg];
   const uint4* s128 = (const uint4*)(sig + (size_t)gg * MOCHI_RSA_BYTES);
 #pragma unroll
   for (int q = 0; q < 16; q++) o.sr[q] = s128[q];
@@ -66,15 +108,23 @@ __device__ __forceinline__ void final_load(uint32_t slot, uint32_t g_lead, const
   }
 }
 
+// Issued after the operands have landed (o.d with them): the digest arrives
+// while the product runs.
+__device__ __forceinline__ void final_load_digest(const uint32_t* __restrict__ digest, uint32_t n_dist, FinalOps& o) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.hw[i] = digest[(size_t)(7 - i) * n_dist + o.d];
+}
+
 // One wave's worth of grants from their loaded operands.
 __device__ __forceinline__ void final_slot(FinalOps& o, uint32_t key, uint32_t g_lead,
                                            const KeyEntry* __restrict__ keys, const FoldKey* __restrict__ fold,
-                                           const uint32_t* __restrict__ digest, uint32_t n_grants,
-                                           uint8_t* __restrict__ flags, const v4i* w) {
+                                           const uint32_t* __restrict__ digest, const uint32_t* __restrict__ lead,
+                                           uint32_t n_dist, uint8_t* __restrict__ flags, const v4i* w,
+                                           FStamps& st) {
   const uint32_t g = o.g;
   const bool active = g != 0xFFFFFFFFu;
   if (__ballot(active) == 0) return;  // this wave's part of the group is padding
-  const uint32_t gg = active ? g : g_lead;  // inactive lanes shadow the lead grant (never stored)
+  const uint64_t t1 = fstamp();
   const KeyEntry* ke = keys + key;
   const cptr n = as_const(ke->n);
   uint32_t sv[kL];
@@ -99,12 +149,11 @@ __device__ __forceinline__ void final_slot(FinalOps& o, uint32_t key, uint32_t g
   // ---- t = z * s: one level of Karatsuba (kara_dev.h), t_hi biased ----
   uint32_t t[2 * kL];
   kara_product(x, sv, t);
+  const uint64_t t2 = fstamp();
   // digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
   uint32_t hl[kHL];
   {
-    uint32_t hw[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) hw[i] = digest[(size_t)(7 - i) * n_grants + gg];
+    const uint32_t (&hw)[8] = o.hw;
 #pragma unroll
     for (int j = 0; j < kHL; j++) {
       const int bit = j * kLimbBits, wi = bit >> 5, sh = bit & 31;
@@ -114,6 +163,7 @@ __device__ __forceinline__ void final_slot(FinalOps& o, uint32_t key, uint32_t g
   }
   // ---- D = t_lo + fold(t_hi) + cadd + n - Cpad - H ----
   fold_reduce<true, true>(t, x, w + (threadIdx.x & 63), as_const(fold[key].cnc), hl);
+  const uint64_t t3 = fstamp();
   // ---- D' = (D + m n) / 2^28 == n ? ----
   cptr nn = n;
   asm volatile("" : "+s"(nn));  // reload n here (kept from the s < n check it would sit in SGPRs and spill)
@@ -130,8 +180,17 @@ __device__ __forceinline__ void final_slot(FinalOps& o, uint32_t key, uint32_t g
   diff |= c != (uint64_t)nn[kL - 1] ? 1u : 0u;
   if (active) {
     const bool ok = s_lt_n && diff == 0;
-    flags[g] = flags[g] | (ok ? MOCHI_GRANT_SIG_OK : 0);
+    flags[g] = (uint8_t)(o.fl | (ok ? MOCHI_GRANT_SIG_OK : 0));
   }
+#if MOCHI_FINAL_STAMPS
+  const uint64_t t4 = fstamp();
+  st.prod += t2 - t1;
+  st.fold += t3 - t2;
+  st.check += t4 - t3;
+  st.n++;
+#else
+  (void)t1, (void)t2, (void)t3, (void)st;
+#endif
 }
 
 // 256 threads (one wave per SIMD, 512 registers: z, s and the whole product
@@ -142,9 +201,12 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
                                                        const KeyEntry* __restrict__ keys,
                                                        const FoldKey* __restrict__ fold,
                                                        const uint32_t* __restrict__ zin,
-                                                       const uint32_t* __restrict__ digest, uint32_t n_grants,
+                                                       const uint32_t* __restrict__ digest,
+                                                       const uint32_t* __restrict__ lead, uint32_t n_dist,
                                                        uint8_t* __restrict__ flags, uint32_t* __restrict__ ctr) {
   __shared__ v4i w[kFoldImgBytes / 16];
+  FStamps st;
+  const uint64_t t_begin = fstamp();
   for_groups(perm, n_slots, signer, fold, w, [&](uint32_t base, uint32_t key, uint32_t g_lead) {
     // (the next half's operands loaded while this half computes -- into AGPRs,
     // 445 registers, or both halves up front, 483 -- measured 10 % and 18 %
@@ -152,15 +214,38 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
 #pragma unroll 1
     for (uint32_t h = 0; h < kBucketAlign; h += 256) {
       FinalOps o;
-      final_load(base + h + threadIdx.x, g_lead, perm, n_slots, sig, zin, o);
-      final_slot(o, key, g_lead, keys, fold, digest, n_grants, flags, w);
+      const uint64_t t0 = fstamp();
+      final_load(base + h + threadIdx.x, g_lead, perm, n_slots, sig, zin, lead, flags, o);
+#if MOCHI_FINAL_STAMPS == 2 || (MOCHI_FINAL_WAIT && !MOCHI_FINAL_STAMPS)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      final_load_digest(digest, n_dist, o);
+#if MOCHI_FINAL_STAMPS
+      st.load += fstamp() - t0;
+#endif
+      (void)t0;
+      final_slot(o, key, g_lead, keys, fold, digest, lead, n_dist, flags, w, st);
     }
   }, MOCHI_FINAL_DYN ? ctr : nullptr);
+#if MOCHI_FINAL_STAMPS
+  const uint64_t t_end = fstamp();
+  const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if ((threadIdx.x & 63) == 0 && wv < 4096) {
+    g_final_stamps[wv][0] = st.load;
+    g_final_stamps[wv][1] = st.prod;
+    g_final_stamps[wv][2] = st.fold;
+    g_final_stamps[wv][3] = st.check;
+    g_final_stamps[wv][4] = st.n;
+    g_final_stamps[wv][5] = t_end - t_begin;
+  }
+#else
+  (void)t_begin;
+#endif
 }
 
 }  // namespace
 
-void launch_rsa_final(const LaunchArgs& a, hipStream_t st) {
+void launch_rsa_final(const LaunchArgs& a, const uint32_t* lead, uint32_t n_dist, hipStream_t st) {
   if (a.dbg_y) {  // mochi_rsa_public_op: materialise s^65537 mod n
     launch_rsa_raw(a, st);
     return;
@@ -168,7 +253,17 @@ void launch_rsa_final(const LaunchArgs& a, hipStream_t st) {
   const uint32_t blocks = fold_grid(a.n_slots);
   if (!blocks) return;
   hipLaunchKernelGGL(k_rsa_final, dim3(blocks), dim3(256), 0, st, a.perm, a.n_slots, a.sig, a.signer, a.keys, a.fold,
-                     a.xbuf, a.digest, a.n_grants, a.flags, a.total + kTotFinalGroup);
+                     a.xbuf, a.digest, lead, n_dist, a.flags, a.total + kTotFinalGroup);
 }
 
 }  // namespace mochi
+
+#if MOCHI_FINAL_STAMPS
+extern "C" int mochi_debug_final_stamps(unsigned long long* out, unsigned n_waves) {
+  if (n_waves > 4096) n_waves = 4096;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mochi::g_final_stamps), 48 * (size_t)n_waves, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif
