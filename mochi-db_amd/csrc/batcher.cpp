@@ -81,8 +81,8 @@ struct Flusher {
   std::vector<uint32_t> accept, op_g0;
   std::vector<int64_t> op_ts;
   // when this flusher's last batch completed (under the batcher's mu, before its
-  // callers were woken): the queue length then and the batch's size
-  size_t q_at_done = 0, last_n = 0;
+  // callers were woken): the batcher's arrival count then and the batch's size
+  uint64_t arr_at_done = 0, last_n = 0;
   std::chrono::steady_clock::time_point t_done;
 };
 
@@ -104,7 +104,10 @@ struct mochi_batcher {
   uint32_t live = 0;             // flusher threads still in run()
   uint32_t waiters = 0;          // blocking callers not yet out of their wait (mu is theirs until then)
   uint64_t n_batches = 0, n_msgs = 0;
-  uint32_t collecting = 0;  // flushers waiting for the callers their last batch released (take())
+  uint64_t n_arrived = 0;  // requests ever enqueued (take(): arrivals since a flusher's last completion)
+  uint32_t collecting = 0;  // flushers waiting for the callers their last batch released
+  uint32_t in_flight = 0;   // batches taken and not yet completed
+  static constexpr size_t kConcurrentMin = 64;
   std::vector<Flusher> fl;
 
   // Frees the flushers' pinned buffers, then lets the contexts go: however the
@@ -118,9 +121,9 @@ struct mochi_batcher {
   }
 
   // Takes the next batch.  Waits for work; then, if this flusher has just
-  // completed a batch, until the callers that batch released are back (the
-  // queue holds what it held at completion plus that batch's size) or
-  // max_wait_us after the completion: blocking callers resubmit within
+  // completed a batch, until the callers that batch released are back (as many
+  // requests arrived since the completion as the batch held, whichever flusher
+  // they went to) or max_wait_us after the completion: blocking callers resubmit within
   // microseconds of their verdicts, and taking the first of them alone would
   // split them into alternating batches that each wait for the other's flight
   // (2 blocking workers on one context: every request paid two GPU round
@@ -129,24 +132,35 @@ struct mochi_batcher {
   bool take(Flusher& f, std::vector<Request*>& batch) {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      // an idle flusher leaves the queue to a sibling that is collecting its callers
-      cv_work.wait(lk, [&] { return stop || (!q.empty() && (f.last_n || collecting == 0 || q.size() >= max_msgs)); });
-      if (q.empty()) return false;  // stopped and drained
-      if (f.last_n) {
-        const size_t want = f.q_at_done + f.last_n < max_msgs ? f.q_at_done + f.last_n : max_msgs;
+      // Small batches go to the GPU one at a time: two in flight at once on one
+      // GPU took about twice as long each (2 blocking workers on 2 contexts: p50
+      // 945 us vs 555 us on one), so a flusher takes work while a sibling's batch
+      // is in flight only once kConcurrentMin requests wait (load that fills
+      // several contexts), and an idle flusher leaves arrivals to a sibling that
+      // is collecting the callers its batch released.
+      auto may_take = [&] { return in_flight == 0 || q.size() >= kConcurrentMin || q.size() >= max_msgs; };
+      cv_work.wait(lk, [&] {
+        return stop || (!q.empty() && (f.last_n || collecting == 0 || q.size() >= max_msgs) && may_take());
+      });
+      if (q.empty()) {  // stopped and drained
+        if (f.last_n) collecting--, f.last_n = 0;
+        return false;
+      }
+      if (f.last_n) {  // a collector since its batch completed (run(): collecting++ under mu)
         const auto deadline = f.t_done + std::chrono::microseconds(max_wait_us);
-        collecting++;
-        while (!stop && !q.empty() && q.size() < want) {
+        while (!stop && !q.empty() && q.size() < max_msgs && n_arrived - f.arr_at_done < f.last_n) {
           if (std::chrono::steady_clock::now() >= deadline) break;
           cv_work.wait_until(lk, deadline);
         }
         collecting--;
         f.last_n = 0;
+        if (collecting == 0) cv_work.notify_all();  // idle siblings may take what this batch leaves
       }
-      if (q.empty()) continue;  // a sibling flusher took it: never verify M = 0
+      if (q.empty() || !may_take()) continue;  // a sibling took it (never verify M = 0), or one is in flight
       const size_t n = q.size() < max_msgs ? q.size() : max_msgs;
       batch.assign(q.begin(), q.begin() + n);
       q.erase(q.begin(), q.begin() + n);
+      in_flight++;
       if (!q.empty()) cv_work.notify_one();  // leave the rest to an idle sibling now
       return true;
     }
@@ -165,15 +179,22 @@ struct mochi_batcher {
         if (r->cb) owned.push_back(r);
       {
         std::lock_guard<std::mutex> lk(mu);
+        // the callers this batch releases: its blocking ones (a completion
+        // callback that resubmits has done so already, above)
+        size_t blocking = 0;
+        for (Request* r : batch) blocking += r->cb ? 0 : 1;
         for (Request* r : batch)
           if (!r->cb) r->done = true;
         n_batches++;
         n_msgs += batch.size();
-        f.q_at_done = q.size();
-        f.last_n = batch.size();
+        f.arr_at_done = n_arrived;
+        f.last_n = blocking;
+        in_flight--;
+        if (blocking) collecting++;  // until take() has collected them: idle siblings hold back
         f.t_done = std::chrono::steady_clock::now();
       }
       cv_done.notify_all();
+      cv_work.notify_all();  // siblings holding back while this batch was in flight
       for (Request* r : owned) delete r;
     }
     bool last;
@@ -290,9 +311,10 @@ struct mochi_batcher {
 
   void enqueue(Request* r) {  // mu held
     q.push_back(r);
+    n_arrived++;
     // every waiting flusher re-checks: a collecting one counts the arrival, an idle
-    // one takes the queue unless a sibling is collecting (notify_one could wake
-    // an idle flusher that then waits on, and the collector would sleep to its deadline)
+    // one takes the queue (notify_one could wake only the idle one, which takes
+    // the request, while the collector sleeps on to its deadline)
     cv_work.notify_all();
   }
 };

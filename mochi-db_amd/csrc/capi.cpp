@@ -872,6 +872,10 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
     auto down = [&](size_t off, size_t bytes) -> hipError_t {
       return bytes ? hipMemcpyAsync(pout + off, dout + off, bytes, hipMemcpyDeviceToHost, c->s_out) : hipSuccess;
     };
+    if (nchunks == 1 && out_total <= (4u << 20)) {  // one small chunk: one download of the whole region
+      HIP_TRY(down(0, out_total));
+      continue;
+    }
     const size_t ng = k.g1 - k.g0, nc = k.c1 - k.c0, no = k.o1 - k.o0;
     const size_t acc_words = j + 1 == nchunks ? nbits_c / 4 - k.c0 / 32 : nc / 32;
     if (o->grant_flags) HIP_TRY(down(o_flags + k.g0, ng));
@@ -1470,8 +1474,12 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   hipStream_t st = c->stream;
   // sources already in pinned memory (mochi_host_alloc) are DMA'd in place;
   // the rebased op_flags_off CSR (segment 3) is always staged
+  // One small chunk (a batcher flush): every segment staged and ONE upload and
+  // ONE download of the whole region -- a copy costs ~5 us of its own on the
+  // GPU whatever its size, and a 2-message batch moved 5 + 7 of them.
+  const bool one_copy = nch == 1 && in_total <= (4u << 20);
   bool pinned[7];
-  for (int i = 0; i < 7; i++) pinned[i] = i != 3 && is_pinned(seg_src(ch[0], i));
+  for (int i = 0; i < 7; i++) pinned[i] = !one_copy && i != 3 && is_pinned(seg_src(ch[0], i));
   std::vector<mochi_write2_batch> dws(nch);
   std::vector<mochi::W2Args> args(nch);
   HIP_TRY(scratch_acquire(c, st));
@@ -1499,6 +1507,7 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     auto down = [&](size_t off, size_t bytes) -> hipError_t {
       return bytes ? hipMemcpyAsync(pout + off, dout + off, bytes, hipMemcpyDeviceToHost, c->s_out) : hipSuccess;
     };
+    if (one_copy) return (int)(down(0, out_total) == hipSuccess ? MOCHI_OK : fail(MOCHI_EHIP, "download failed"));
     const size_t no = ofo ? ofo[k.m1] - o0 : 0;
     const size_t acc_words = j + 1 == nch ? nbits / 4 - k.m0 / 32 : nm / 32;
     HIP_TRY(down(o_acc + 4 * (size_t)(k.m0 / 32), 4 * acc_words));
@@ -1517,14 +1526,17 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
       uint32_t* f = (uint32_t*)(pin + k.seg[3]);
       for (uint32_t m = k.m0; m <= k.m1; m++) f[m - k.m0] = ofo[m] - ofo[k.m0];
     }
+    size_t staged_end = 0;
     for (int i = 0; i < 7; i++) {
       const size_t n = seg_bytes(k, i);
       if (!n) continue;
       const void* src = pin + k.seg[i];
       if (pinned[i]) src = seg_src(k, i);  // DMA'd in place (e.g. the batcher's pinned batch)
       else if (i != 3) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
-      HIP_TRY(hipMemcpyAsync(din + k.seg[i], src, n, hipMemcpyHostToDevice, c->s_in));
+      if (one_copy) staged_end = k.seg[i] + n > staged_end ? k.seg[i] + n : staged_end;
+      else HIP_TRY(hipMemcpyAsync(din + k.seg[i], src, n, hipMemcpyHostToDevice, c->s_in));
     }
+    if (one_copy && staged_end) HIP_TRY(hipMemcpyAsync(din, pin, staged_end, hipMemcpyHostToDevice, c->s_in));
     HIP_TRY(hipEventRecord(c->chunk_ev[2 * j], c->s_in));
     mochi_write2_batch& dw = dws[j];
     memset(&dw, 0, sizeof dw);

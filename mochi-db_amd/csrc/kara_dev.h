@@ -156,6 +156,144 @@ __device__ __forceinline__ void kara_square(uint32_t (&x)[kL], uint32_t (&t)[2 *
       [&](auto kc, uint64_t& carry) { return square_col<kKH, decltype(kc)::value>(x, carry); });
 }
 
+#ifndef MOCHI_KARA2
+#define MOCHI_KARA2 0  // A/B (round 6): a second Karatsuba level on x^2's L and H squares
+#endif
+
+// Column K of the square of the N limbs a[AO..AO+N) (28- or 29-bit), product-
+// scanned exactly like square_col (operands doubled in place after their
+// column): K < 2N-1 a column sum, K = 2N-1 and 2N the last carry's two limbs.
+template <int AO, int K, int N, int NA>
+__device__ __forceinline__ uint32_t square_col_n(uint32_t (&a)[NA], uint64_t& carry) {
+  if constexpr (K == 2 * N - 1) {
+    return (uint32_t)carry & kLimbMask;
+  } else if constexpr (K == 2 * N) {
+    return (uint32_t)(carry >> kLimbBits);
+  } else {
+    constexpr int lo = K - N + 1 > 0 ? K - N + 1 : 0;
+    constexpr int xhi = K > 0 ? (K - 1) / 2 : -1;
+    uint64_t acc = carry;
+    static_for<lo, xhi + 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      acc = mad64(a[AO + i], a[AO + K - i], acc);
+      asm volatile("" ::"v"(acc));
+    });
+    if constexpr ((K & 1) == 0) {
+      acc = mad64(a[AO + (K >> 1)], a[AO + (K >> 1)], acc);
+      if constexpr ((K >> 1) < N - 1) a[AO + (K >> 1)] += a[AO + (K >> 1)];
+    }
+    carry = acc >> kLimbBits;
+    return (uint32_t)acc & kLimbMask;
+  }
+}
+
+// The square of the 37 limbs a[AO..AO+37) (28-bit), one more Karatsuba level,
+// streamed column by column in order (col<c>() for c = 0..73, normalised):
+// A = A0 + B' A1 (A0 19 limbs, A1 18, B' = 2^(28*19)), P0 = A0^2, P1 = A1^2,
+// P2 = (A0 + A1)^2 (19 limbs of 29 bits: 190 + 171 + 190 = 551 mads instead of
+// 703), and with R = P0 - B' P1,  A^2_c = R_c + P2_(c-19) - R_(c-19): R is kept
+// for 19 columns, the three chains advance in step, and a running carry
+// normalises the (signed) combination.  `a` is clobbered (doubled in place).
+template <int AO, int NA>
+struct Square2 {
+  static constexpr int N0 = 19, N1 = kKH - N0;  // 19 + 18
+  uint32_t (&a)[NA];
+  uint32_t s[N0];
+  int32_t r[N0];
+  uint64_t c0 = 0, c1 = 0, c2 = 0;
+  int32_t cn = 0;
+  __device__ __forceinline__ explicit Square2(uint32_t (&x)[NA]) : a(x) {
+#pragma unroll
+    for (int i = 0; i < N0; i++) s[i] = a[AO + i] + (i < N1 ? a[AO + N0 + i] : 0u);
+  }
+  template <int C>
+  __device__ __forceinline__ uint32_t col() {
+    int32_t p0 = 0, p1 = 0, p2 = 0;
+    if constexpr (C <= 2 * N0) p0 = (int32_t)square_col_n<AO, C, N0>(a, c0);
+    if constexpr (C - N0 >= 0 && C - N0 <= 2 * N1) p1 = (int32_t)square_col_n<AO + N0, C - N0, N1>(a, c1);
+    if constexpr (C - N0 >= 0 && C - N0 <= 2 * N0) p2 = (int32_t)square_col_n<0, C - N0, N0>(s, c2);
+    const int32_t rc = p0 - p1;
+    int32_t v = rc + p2 + cn;
+    if constexpr (C >= N0) v -= r[C % N0];
+    r[C % N0] = rc;
+    cn = v >> kLimbBits;  // arithmetic: the combination is signed
+    return (uint32_t)v & kLimbMask;
+  }
+};
+
+// MOCHI_KARA2 == 4: kara_square's lockstep Q-form with L by Square2.
+__device__ __forceinline__ void kara_square2_lockstep(uint32_t (&x)[kL], uint32_t (&t)[2 * kL]) {
+  {  // M = (x_lo + x_hi)^2 -> t[37 + k]
+    uint32_t sx[kKH];
+#pragma unroll
+    for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
+    kara_middle(t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(sx, carry); });
+  }
+  Square2<0, kL> lo(x);
+#if MOCHI_KARA2 == 5  // both L and H by Square2
+  Square2<kKH, kL> hi(x);
+  kara_combine(
+      t, [&](auto kc, uint64_t&) { return lo.template col<decltype(kc)::value>(); },
+      [&](auto kc, uint64_t&) { return hi.template col<decltype(kc)::value>(); });
+#else
+  kara_combine(
+      t, [&](auto kc, uint64_t&) { return lo.template col<decltype(kc)::value>(); },
+      [&](auto kc, uint64_t& carry) { return square_col<kKH, decltype(kc)::value>(x, carry); });
+#endif
+}
+
+// kara_square with L and H by Square2, combined directly (t[c] += L_c,
+// t[37+c] -= L_c; then t[37+m] -= H_m, t[74+m] += H_m): the same t as
+// kara_square's lockstep Q-form, with one inner square's state live at a time.
+__device__ __forceinline__ void kara_square2(uint32_t (&x)[kL], uint32_t (&t)[2 * kL]) {
+  {  // M = (x_lo + x_hi)^2 -> t[37 + k]
+    uint32_t sx[kKH];
+#pragma unroll
+    for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
+    kara_middle(t, [&](auto kc, uint64_t& carry) { return square_col<0, decltype(kc)::value>(sx, carry); });
+  }
+  {
+#if MOCHI_KARA2 == 3  // (diagnostic) the direct combination with one level for both
+    uint64_t cl = 0;
+#else
+    Square2<0, kL> lo(x);
+#endif
+    static_for<0, kL>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+#if MOCHI_KARA2 == 3
+      const uint32_t l = square_col<0, c>(x, cl);
+#else
+      const uint32_t l = lo.template col<c>();
+#endif
+      if constexpr (c < kKH) t[c] = l;
+      else t[c] += l;
+      t[kKH + c] -= l;
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  {
+#if MOCHI_KARA2 >= 2  // the second level for L only (H one level, square_col)
+    uint64_t ch = 0;
+#else
+    Square2<kKH, kL> hi(x);
+#endif
+    static_for<0, kL>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+#if MOCHI_KARA2 >= 2
+      const uint32_t h = square_col<kKH, m>(x, ch);
+#else
+      const uint32_t h = hi.template col<m>();
+#endif
+      t[kKH + m] -= h;
+      if constexpr (m <= kKH) t[kL + m] += h;
+      else t[kL + m] = h;
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+#pragma unroll
+  for (int k = kFoldF; k < 2 * kL; k++) t[k] ^= kFoldBias;
+}
+
 // t = x * y as 148 limbs (k_rsa_final), the same layout as kara_square.
 __device__ __forceinline__ void kara_product(const uint32_t (&x)[kL], const uint32_t (&y)[kL], uint32_t (&t)[2 * kL]) {
   {  // M = (x_lo + x_hi)(y_lo + y_hi) -> t[37 + k]

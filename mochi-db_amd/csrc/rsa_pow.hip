@@ -179,7 +179,13 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
       asm volatile("" : "+s"(ci));  // keep the 74 cadd loads inside the loop (SGPR pressure if hoisted)
       uint32_t t[2 * kL];
       const uint64_t t0 = stamp();
+#if MOCHI_KARA2 >= 4
+      kara_square2_lockstep(x, t);  // A/B: the second level for L in the lockstep form
+#elif MOCHI_KARA2
+      kara_square2(x, t);  // A/B: two Karatsuba levels for L and H (kara_dev.h)
+#else
       kara_square(x, t);  // t = x^2, Karatsuba, t_hi biased (kara_dev.h)
+#endif
       const uint64_t t1 = stamp();
       phase_barrier();
       __builtin_amdgcn_s_setprio(1);
