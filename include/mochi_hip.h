@@ -294,6 +294,13 @@ int mochi_ctx_last_total_ms(mochi_ctx* ctx, float* total_ms);
  * or 262144).  Chunks always hold whole certificates, 32 at a time. */
 int mochi_ctx_set_chunk_grants(mochi_ctx* ctx, uint32_t grants);
 
+/* Small-batch launch sequence (a batcher flush of a few messages): a batch of
+ * at most `grants` grants is bucketed by one kernel and prepped grant by grant
+ * on the launch stream, instead of the large-batch sequence (three bucketing
+ * kernels, the certificate-level grant dedup forked beside k_rsa_pow).  Same
+ * outputs either way.  Default 4096; 0 = always the large-batch sequence. */
+int mochi_ctx_set_small_batch(mochi_ctx* ctx, uint32_t grants);
+
 /*
  * Pinned (page-locked) host memory for building batches in place: arrays of a
  * mochi_batch that live in such memory are DMA'd straight to the device by

@@ -284,6 +284,7 @@ struct mochi_ctx {
   float last_ms[3] = {0, 0, 0};  // first upload, compute span, last download of the last host-path call
   float last_total_ms = 0;       // whole pipelined host-path call (first H2D start -> last D2H end)
   uint32_t chunk_grants = 0;     // host-path chunk target (grants), mochi_ctx_set_chunk_grants
+  uint32_t small_grants = 4096;  // small-batch launch sequence up to this many grants (mochi_ctx_set_small_batch)
   // Write2 wire path: server-id table + decode scratch
   DevBuf ids, id_off;
   uint32_t n_ids = 0;
@@ -592,6 +593,7 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.perm = c->perm.as<uint32_t>();
   a.xbuf = c->xbuf.as<uint32_t>();
   a.rare = c->dedup.as<uint8_t>();
+  a.small_grants = c->small_grants;
   a.grant_same = grant_same;
   a.grant_valid_bits = o->grant_valid_bits;
   a.cert_accept_bits = o->cert_accept_bits;
@@ -1122,6 +1124,13 @@ void* mochi_host_alloc(uint64_t bytes) {
 
 void mochi_host_free(void* ptr) {
   if (ptr) (void)hipHostFree(ptr);
+}
+
+int mochi_ctx_set_small_batch(mochi_ctx* c, uint32_t grants) {
+  if (!c) return fail(MOCHI_EINVAL, "null context");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->small_grants = grants;
+  return MOCHI_OK;
 }
 
 int mochi_ctx_set_chunk_grants(mochi_ctx* c, uint32_t grants) {

@@ -59,6 +59,7 @@ struct LaunchArgs {
   // mochi_rsa_public_op only: raw s^65537 mod n words [N][64] (else null)
   uint32_t* dbg_y;
   bool skip_prep_tally;
+  uint32_t small_grants;  // small-batch launch sequence for N <= this (0: never)
   // grant prep runs on `aux` (forked from / joined back to the launch stream
   // with ev_fork / ev_join) beside k_rsa_pow; null = serial on the launch stream
   hipStream_t aux;

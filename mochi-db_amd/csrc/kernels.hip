@@ -446,6 +446,56 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint16_t* __restri
     if (s[j] != 0xFFFFFFFFu) perm[lbase[s[j]] + rank[j]] = i0 + j * blockDim.x;
 }
 
+// A small batch (a batcher flush: a few messages) in ONE kernel of one block:
+// perm cleared, counts, bucket starts, totals and the scatter -- instead of two
+// memsets and three kernels, each ~5 us of dispatch on an otherwise idle GPU.
+constexpr uint32_t kSmallGrants = 4096;
+
+__global__ __launch_bounds__(1024) void k_bucket_small(const uint16_t* __restrict__ signer, uint32_t n, uint32_t n_keys,
+                                                       uint32_t n_slots, uint32_t* __restrict__ perm,
+                                                       uint32_t* __restrict__ total) {
+  extern __shared__ uint32_t lds[];  // [n_keys] count, then [n_keys] cursor
+  uint32_t* cnt = lds;
+  uint32_t* cur = lds + n_keys;
+  __shared__ uint32_t part[1024];
+  for (uint32_t k = threadIdx.x; k < n_keys; k += blockDim.x) cnt[k] = 0;
+  for (uint32_t i = threadIdx.x; i < n_slots; i += blockDim.x) perm[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t k = signer[i];
+    if (k < n_keys) atomicAdd(&cnt[k], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of the 512-aligned bucket sizes: per-thread runs, then thread 0 over the 1024 partials
+  const uint32_t per = (n_keys + blockDim.x - 1) / blockDim.x, b = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t k = b; k < b + per && k < n_keys; k++) sum += (cnt[k] + kBucketAlign - 1) & ~(kBucketAlign - 1);
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (uint32_t t = 0; t < blockDim.x; t++) {
+      const uint32_t v = part[t];
+      part[t] = run;
+      run += v;
+    }
+    total[0] = run;
+#pragma unroll
+    for (int i = 1; i < kTotalWords; i++) total[i] = 0;  // the counters of this call's later kernels (kernels.h)
+  }
+  __syncthreads();
+  uint32_t run = part[threadIdx.x];
+  for (uint32_t k = b; k < b + per && k < n_keys; k++) {
+    cur[k] = run;
+    run += (cnt[k] + kBucketAlign - 1) & ~(kBucketAlign - 1);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t k = signer[i];
+    if (k < n_keys) perm[atomicAdd(&cur[k], 1u)] = i;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Certificate tally (lane = certificate).  Restates oracle_tally, i.e.
 // InMemoryDataStore.java:613-640 then :576-611 (verdict part).
@@ -784,6 +834,15 @@ static bool dedup_off() {
   return off;
 }
 
+// MOCHI_NO_SMALL=1 (A/B): small batches take the large-batch launch sequence
+static bool small_off() {
+  static const bool off = [] {
+    const char* e = getenv("MOCHI_NO_SMALL");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
 // MOCHI_PREP_FIRST=1 (A/B): grant prep ahead of k_rsa_pow on the main stream
 static bool prep_first() {
   static const bool on = [] {
@@ -818,19 +877,25 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   // per SIMD-half, nothing to hide its latency) it cost the step 5-9 ms
   // (DESIGN.md section 9).  The fork comes after bucketing: beside prep, the
   // short bucket kernels (which gate k_rsa_pow) took ~4x longer.
+  // A small batch (<= kSmallGrants): one bucketing kernel, then the per-grant prep
+  // on the launch stream -- no fork, no dedup passes (each a dispatch of its own)
+  const bool small = N && N <= a.small_grants && N <= kSmallGrants && !small_off();
   // grant dedup (k_grant_prep_cert + k_grant_prep_rare): results stored once per distinct
   // grant, read through `lead`; without it every grant is its own distinct index
-  const bool dedup = a.rare && a.lead && a.cert_grant_off && C && !dedup_off();
+  const bool dedup = !small && a.rare && a.lead && a.cert_grant_off && C && !dedup_off();
   const uint32_t nd = a.n_dist ? a.n_dist : N;
   const PrepArgs pa{a.blob,     a.grant_off, a.grant_len, N,        nd,      dedup ? C : 0u,
                     a.digest,   a.ts,        a.hash_off,  a.hash_len, a.flags, dedup ? a.lead : nullptr};
   const uint32_t* lead = dedup ? a.lead : nullptr;
   const bool prep = N && !a.skip_prep_tally;
-  const bool fork = prep && a.aux;
+  const bool fork = prep && a.aux && !small;
   hipStream_t ps = fork ? a.aux : st;
   auto bucket = [&](hipStream_t bs) -> hipError_t {
     mark(kStageBucket, false, bs);
-    if (N) {
+    if (small) {
+      hipLaunchKernelGGL(k_bucket_small, dim3(1), dim3(1024), 2 * sizeof(uint32_t) * a.n_keys, bs, a.signer, N,
+                         a.n_keys, a.n_slots, a.perm, a.total);
+    } else if (N) {
       hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, bs);
       if (e != hipSuccess) return e;
       e = hipMemsetAsync(a.perm, 0xFF, sizeof(uint32_t) * (size_t)a.n_slots, bs);

@@ -175,6 +175,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mochi_write1_classify_device.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mochi_ctx_last_total_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     lib.mochi_ctx_set_chunk_grants.argtypes = [vp, u32]
+    lib.mochi_ctx_set_small_batch.argtypes = [vp, u32]
     lib.mochi_ctx_set_server_ids.argtypes = [vp, vp, vp, u32]
     lib.mochi_verify_write2.argtypes = [vp, vp, vp, vp, vp]
     lib.mochi_verify_write2_device.argtypes = [vp, vp, vp, vp, vp, vp]
@@ -535,6 +536,12 @@ class Verifier:
                    op_key_off=arr(d.op_key_off, O, np.uint64), op_key_len=arr(d.op_key_len, O, np.uint32))
         self.lib.mochi_write2_decoded_free(ctypes.addressof(d))
         return out
+
+    def set_small_batch(self, grants: int) -> None:
+        """Batches of at most `grants` grants take the small-batch launch sequence
+        (mochi_ctx_set_small_batch); 0 = never."""
+        if self.lib.mochi_ctx_set_small_batch(self.ctx, int(grants)) != OK:
+            raise MochiError(_err(self.lib))
 
     def set_chunk_grants(self, grants: int) -> None:
         """Host-path pipeline chunk target (grants); 0 restores the default."""

@@ -458,11 +458,21 @@ def test_grant_group_depth_matches_google_protobuf(pool4, ver4, golden_dir):
             assert g.grant_ts[i] == v["expect"]["timestamp"], v["name"]
 
 
+_SIG_CACHE = {}
+
+
+def _sign_cached(pem, gb):
+    key = (pem, gb)
+    if key not in _SIG_CACHE:
+        _SIG_CACHE[key] = O.rsa_sign(pem, gb)
+    return _SIG_CACHE[key]
+
+
 def _dedup_batch(pems, certs, shared_first=False):
     """certs: list of lists of (grant bytes, signer, key slot); every grant its own copy
-    in the blob at a varying alignment (the byte-compare path of k_grant_dedup), or --
-    with shared_first -- grants equal to the certificate's first one pointing at its
-    bytes (the SoA layout's offset shortcut)."""
+    in the blob at a varying alignment (the byte compares of k_grant_prep_cert /
+    k_grant_match), or -- with shared_first -- grants equal to the certificate's first
+    one pointing at its bytes (the SoA layout's offset shortcut)."""
     blob = bytearray(b"\x07")
     offs, lens, sigs, signer, gkey, cgo = [], [], [], [], [], [0]
     cop, opk = [0], []
@@ -478,7 +488,7 @@ def _dedup_batch(pems, certs, shared_first=False):
                 if first is None:
                     first = (gb, offs[-1])
             lens.append(len(gb))
-            sigs.append(O.rsa_sign(pems[s], gb))
+            sigs.append(_sign_cached(pems[s], gb))
             signer.append(s)
             gkey.append(k)
         cgo.append(len(offs))
@@ -495,14 +505,26 @@ def _dedup_batch(pems, certs, shared_first=False):
                     expected_hash=np.stack([np.frombuffer(th.encode(), np.uint8)] * C))
 
 
+@pytest.fixture
+def dedup_path(ver4):
+    """The large-batch launch sequence (certificate-level dedup) even for these small
+    test batches; the small-batch sequence is restored afterwards."""
+    ver4.set_small_batch(0)
+    yield ver4
+    ver4.set_small_batch(4096)
+
+
 @pytest.mark.parametrize("shared_first", [False, True])
-def test_grant_dedup_one_byte_differences(pool4, ver4, shared_first):
+@pytest.mark.parametrize("small", [False, True])
+def test_grant_dedup_one_byte_differences(pool4, ver4, shared_first, small):
     """Grant prep hashes each distinct grant of a (certificate, key slot) once
-    (k_grant_dedup + k_grant_prep_lead).  Grants that differ from the slot's first
+    (k_grant_prep_cert, k_grant_match, k_grant_prep_rare; `small`: the small-batch
+    sequence, every grant on its own).  Grants that differ from the slot's first
     grant in exactly one byte -- timestamp skew, a g1 / g0 transactionHash mismatch, a
     flipped objectId byte, a trailing unknown field -- must be prepped on their own:
     flags, timestamps and verdicts bit-exact with the oracle (which hashes every
     grant)."""
+    ver4.set_small_batch(4096 if small else 0)
     pems = W.load_keys(4)
     th = W.txn_hash_hex(9)
     oth = th[:-1] + ("0" if th[-1] != "0" else "1")
@@ -526,15 +548,45 @@ def test_grant_dedup_one_byte_differences(pool4, ver4, shared_first):
         g = ver4.verify(b, 4, strict)
         o = O.verify_batch(pool4.moduli, b, 4, strict, 2)
         assert_same(g, o, f"strict={strict}")
+    ver4.set_small_batch(4096)
     assert (g.grant_flags & 1).all()  # every signature is valid
     reasons = {k: int(g.cert_reason[i]) for i, k in enumerate(variants)}
     assert reasons["honest"] == mh.ACCEPT and reasons["ts_skew"] == mh.REJECT_TS_MISMATCH
     assert reasons["g0_hash"] == mh.REJECT_HASH_MISMATCH
 
 
-def test_grant_dedup_large_certificate(pool4, ver4):
-    """A certificate above k_grant_dedup's slot-scan bound (256 grants) is prepped grant
-    by grant; results equal the oracle's."""
+@pytest.mark.parametrize("shared_first", [False, True])
+def test_grant_dedup_block_over_lds_and_third_slot(pool4, dedup_path, shared_first):
+    """k_grant_prep_cert's edges: a block of 256 certificates holding more than
+    kPrepBlockGrants (2048) grants stores its results lane by lane (no LDS staging, so
+    no k_grant_match: byte compares in the certificate's lane), a second block within
+    the bound is staged, and certificates with three key slots leave the third slot's
+    grants to k_grant_prep_rare -- each with one-byte variants in every slot.  ==
+    the oracle."""
+    pems = W.load_keys(4)
+    th = W.txn_hash_hex(9)
+    g = [[W.encode_grant(f"DEMO_KEY_SLOT{j}", 1000 + 10 * j + d, th) for d in (0, 1)] for j in range(3)]
+    certs = []
+    for c in range(512):
+        cert = []
+        for r in range(4):
+            for j in range(3 if c < 256 else 2):  # block 0: 256 x 12 grants > 2048; block 1: 256 x 8
+                skew = (c + j) % 7 == 0 and r == 2  # one replica's grant of the slot differs in one byte
+                cert.append((g[j][1 if skew else 0], r, j))
+        certs.append(cert)
+    b = _dedup_batch(pems, certs, shared_first)
+    assert int(b.cert_grant_off[256]) > 2048 and int(b.cert_grant_off[512] - b.cert_grant_off[256]) <= 2048
+    for strict in (True, False):
+        got = dedup_path.verify(b, 4, strict)
+        o = O.verify_batch(pool4.moduli, b, 4, strict, 4)
+        assert_same(got, o, f"strict={strict}")
+    assert (got.cert_reason == mh.REJECT_TS_MISMATCH).any() and (got.cert_reason == mh.ACCEPT).any()
+
+
+def test_grant_dedup_large_certificate(pool4, dedup_path):
+    """A certificate of 300 grants (a 64-bit slot mask is not involved: one key; more
+    grants than any wave) and a small one: results equal the oracle's."""
+    ver4 = dedup_path
     pems = W.load_keys(4)
     th = W.txn_hash_hex(9)
     gs = [W.encode_grant("DEMO_KEY_BIG", 1000 + (i % 3 == 2), th) for i in range(300)]
