@@ -939,7 +939,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     if (e == hipSuccess) e = hipStreamWaitEvent(st, a.ev_join, 0);
     if (e != hipSuccess) return e;
     mark(kStagePow, false, st);
-    if (N) launch_rsa_pow(a, st);
+    if (N) launch_rsa_pow(a, st, small);
     mark(kStagePow, true, st);
   } else {
     hipError_t e = bucket(st);
@@ -956,7 +956,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
       if (e != hipSuccess) return e;
     }
     mark(kStagePow, false, st);
-    if (N) launch_rsa_pow(a, st);
+    if (N) launch_rsa_pow(a, st, small);
     mark(kStagePow, true, st);
     if (fork) {
       e = hipStreamWaitEvent(st, a.ev_join, 0);

@@ -39,6 +39,8 @@
 #include "fold_dev.h"
 #include "rsa_common.h"
 
+#include <cstdlib>
+
 // MOCHI_POW_STAMPS (measurement builds only, `make ab`): per wave, s_memtime
 // cycles spent in x^2, in the fold, and in the whole kernel, read back with
 // mochi_debug_pow_stamps() (scripts/pow_stamps.py)
@@ -222,6 +224,102 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// k_rsa_pow_lat — the same 16 squarings for a SMALL batch (a batcher flush of a
+// few messages), where the chain's latency is the cost: one signature's chain
+// runs on one lane, 16 x (x^2 17.3k + fold 10.6k cycles) in k_rsa_pow, and the
+// other waves of its group are padding.  Here a block of 4 waves owns one
+// 64-slot chunk, and each squaring's three Karatsuba squares run on three
+// SIMDs at once: wave 0 L = x_lo^2 (kept in registers), wave 1 H = x_hi^2 and
+// wave 2 M = (x_lo + x_hi)^2 (written to LDS); wave 0 combines them (kara_dev.h
+// kara_combine) and folds (fold_dev.h), and writes the new x to LDS for waves 1
+// and 2.  Two block barriers per squaring; the same arithmetic, limb for limb,
+// as k_rsa_pow (bit-exact by construction and by the parity tests, which run
+// every small batch through it).  One block per CU (the image + 57 KB of
+// exchange), one wave per SIMD.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLatChunk = 64;
+
+__global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
+  __shared__ v4i w[kFoldImgBytes / 16];
+  __shared__ uint32_t xh[kL][kLatChunk];       // H = x_hi^2 (74 limbs)
+  __shared__ uint32_t xm[kL + 1][kLatChunk];   // M = (x_lo + x_hi)^2 (75 limbs)
+  __shared__ uint32_t xn[kL][kLatChunk];       // the folded x for waves 1 and 2
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * kLatChunk;
+  if (base >= a.n_slots) return;
+  // buckets are filled from their start: a chunk whose first slot is empty is all padding
+  const uint32_t g_lead = __builtin_amdgcn_readfirstlane(a.perm[base]);
+  if (g_lead == 0xFFFFFFFFu) return;
+  const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)a.signer[g_lead]);
+  {
+    const v4i* src = (const v4i*)a.fold[key].img;
+    for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
+  }
+  const uint32_t slot = base + lane;
+  const uint32_t g = slot < a.n_slots ? a.perm[slot] : 0xFFFFFFFFu;
+  const bool active = g != 0xFFFFFFFFu;
+  uint32_t x[kL];
+  if (wv < 3) {
+    uint32_t wd[64];
+    load_sig_words(a.sig, active ? g : g_lead, wd);  // inactive lanes shadow the lead grant (never stored)
+    words_to_limbs(wd, x);
+  }
+  __syncthreads();
+  const cptr c = as_const(a.fold[key].cadd);
+#pragma unroll 1
+  for (int it = 0; it < 16; it++) {
+    if (it > 0 && (wv == 1 || wv == 2)) {  // the folded x of the last squaring
+#pragma unroll
+      for (int q = 0; q < kL; q++) x[q] = xn[q][lane];
+    }
+    uint32_t lv[kL];
+    if (wv == 0) {  // L = x_lo^2, normalised, into registers
+      uint64_t carry = 0;
+      static_for<0, kL>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        lv[k] = square_col<0, k>(x, carry);
+      });
+    } else if (wv == 1) {  // H = x_hi^2
+      uint64_t carry = 0;
+      static_for<0, kL>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        xh[k][lane] = square_col<kKH, k>(x, carry);
+      });
+    } else if (wv == 2) {  // M = (x_lo + x_hi)^2
+      uint32_t sx[kKH];
+#pragma unroll
+      for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
+      uint64_t carry = 0;
+      static_for<0, kL + 1>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        xm[k][lane] = square_col<0, k>(sx, carry);
+      });
+    }
+    __syncthreads();
+    if (wv == 0) {
+      cptr ci = c;
+      asm volatile("" : "+s"(ci));
+      uint32_t t[2 * kL];
+#pragma unroll
+      for (int k = 0; k <= kL; k++) t[kKH + k] = xm[k][lane];
+      kara_combine(
+          t, [&](auto kc, uint64_t&) { return lv[decltype(kc)::value]; },
+          [&](auto kc, uint64_t&) { return xh[decltype(kc)::value][lane]; });
+      fold_reduce<false, true>(t, x, w + lane, ci, nullptr);
+      if (it < 15) {
+#pragma unroll
+        for (int q = 0; q < kL; q++) xn[q][lane] = x[q];
+      }
+    }
+    __syncthreads();
+  }
+  if (wv == 0 && active) {
+#pragma unroll
+    for (int q = 0; q < kL; q++) a.zout[(size_t)q * a.n_slots + slot] = x[q];
+  }
+}
+
 }  // namespace
 
 #if MOCHI_POW_STAMPS
@@ -231,9 +329,23 @@ extern "C" int mochi_debug_pow_stamps(unsigned long long* out, unsigned n_waves)
 }
 #endif
 
-void launch_rsa_pow(const LaunchArgs& a, hipStream_t st) {
-  const uint32_t blocks = fold_grid(a.n_slots);
+// MOCHI_NO_LAT=1 (A/B): small batches take k_rsa_pow as well
+static bool lat_off() {
+  static const bool off = [] {
+    const char* e = getenv("MOCHI_NO_LAT");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
+void launch_rsa_pow(const LaunchArgs& a, hipStream_t st, bool latency) {
   const PowArgs pw{a.perm, a.n_slots, a.sig, a.signer, a.fold, a.xbuf, a.total + kTotPowGroup};
+  if (latency && !lat_off()) {  // a small batch: one block per 64-slot chunk (empty chunks exit at once)
+    const uint32_t chunks = (a.n_slots + kLatChunk - 1) / kLatChunk;
+    if (chunks) hipLaunchKernelGGL(k_rsa_pow_lat, dim3(chunks), dim3(256), 0, st, pw);
+    return;
+  }
+  const uint32_t blocks = fold_grid(a.n_slots);
   if (blocks) hipLaunchKernelGGL(k_rsa_pow, dim3(blocks), dim3(kBucketAlign), 0, st, pw);
 }
 
