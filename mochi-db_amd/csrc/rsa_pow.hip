@@ -54,6 +54,12 @@
 #ifndef MOCHI_POW_DYN
 #define MOCHI_POW_DYN 1
 #endif
+#ifndef MOCHI_LAT_RAW
+#define MOCHI_LAT_RAW 0
+#endif
+#ifndef MOCHI_LAT_SEQ_TILES
+#define MOCHI_LAT_SEQ_TILES 0  // A/B: k_rsa_pow_lat's M-tiles one after the other
+#endif
 #ifndef MOCHI_POW_NEXT_AHEAD
 #define MOCHI_POW_NEXT_AHEAD 1  // the next group's index fetched one group ahead (below)
 #endif
@@ -117,13 +123,17 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
   // published at its end, so the atomic's round trip runs under this group's
   // signature loads instead of stalling every wave at the group boundary.
   __shared__ uint32_t s_grp[2];
-  if (threadIdx.x == 0) s_grp[0] = atomicAdd(a.ctr, 1u);
+  // no more groups than blocks: one each, by index -- with the counter a block
+  // that started first could take two groups while another had not started yet
+  // (a 2-message batch's pow took 161 or 338 us depending on the dispatch order)
+  const bool one_each = n_groups <= gridDim.x;
+  if (threadIdx.x == 0) s_grp[0] = one_each ? blockIdx.x : atomicAdd(a.ctr, 1u);
   __syncthreads();
   for (uint32_t it_g = 0;; it_g ^= 1) {
     const uint32_t grp = __builtin_amdgcn_readfirstlane(s_grp[it_g]);
     if (grp >= n_groups) break;
     uint32_t nxt = 0;
-    if (threadIdx.x == 0) nxt = atomicAdd(a.ctr, 1u);
+    if (threadIdx.x == 0) nxt = one_each ? n_groups : atomicAdd(a.ctr, 1u);
 #if !MOCHI_POW_NEXT_AHEAD  // A/B: wait for the fetch here, as every wave did before
     if (threadIdx.x == 0) s_grp[it_g ^ 1] = nxt;
     __syncthreads();
@@ -226,25 +236,168 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
 
 // ---------------------------------------------------------------------------
 // k_rsa_pow_lat — the same 16 squarings for a SMALL batch (a batcher flush of a
-// few messages), where the chain's latency is the cost: one signature's chain
-// runs on one lane, 16 x (x^2 17.3k + fold 10.6k cycles) in k_rsa_pow, and the
-// other waves of its group are padding.  Here a block of 4 waves owns one
-// 64-slot chunk, and each squaring's three Karatsuba squares run on three
-// SIMDs at once: wave 0 L = x_lo^2 (kept in registers), wave 1 H = x_hi^2 and
-// wave 2 M = (x_lo + x_hi)^2 (written to LDS); wave 0 combines them (kara_dev.h
-// kara_combine) and folds (fold_dev.h), and writes the new x to LDS for waves 1
-// and 2.  Two block barriers per squaring; the same arithmetic, limb for limb,
-// as k_rsa_pow (bit-exact by construction and by the parity tests, which run
-// every small batch through it).  One block per CU (the image + 57 KB of
-// exchange), one wave per SIMD.
+// few messages), where the chain's latency is the cost: in k_rsa_pow one
+// signature's chain runs on one wave, and alone on its SIMD that wave spends
+// most of each squaring in the fold's dependent MFMA chains (10 M-tiles x 10
+// K-steps, ~20k cycles per squaring with x^2).  Here a block of 4 waves owns
+// one 64-slot chunk (the same 64 signatures on every wave) and spreads each
+// squaring over the CU's four SIMDs:
+//   x^2:  wave 0 L = x_lo^2 (registers), wave 1 H = x_hi^2, wave 2 M = (x_lo +
+//         x_hi)^2 (both to LDS); wave 0 combines them into t (kara_combine) and
+//         writes t to LDS;
+//   fold: wave w computes M-tiles w, w+4, w+8 (their 32-row weight slices of
+//         the key's image, every wave building the B operands from t_hi), and
+//         writes each of its output limbs' two int32 halves (fold_dev.h: p =
+//         c0 + 2^8 c1 + t_lo + cadd, h = c2 + 2^8 c3) to LDS;
+//   then every wave runs the 74-limb carry chain itself (x' = h 2^16 + p +
+//         carry), so x' needs no broadcast.
+// The limb arithmetic is fold_reduce's, split by tile -- bit-exact with
+// k_rsa_pow by construction, and every small batch of the parity tests runs
+// through it.  Five block barriers per squaring; one block per CU (the image +
+// 38 KB of exchange), one wave per SIMD.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kLatChunk = 64;
+constexpr int kLatRows = 2 * kL + 1;  // 149 rows: H + M, then t (148), then the (p, h) pairs (148)
+
+// The (p, h) halves of output limb q of an M-tile from its accumulators (the
+// MFMA layout: half h of the wave holds limb 2u + h of both N-tiles'
+// signatures; one swap per half turns them into this lane's own limbs)
+template <int MT>
+__device__ __forceinline__ void lat_assemble(const v16i& d0, const v16i& d1, cptr cadd,
+                                             const uint32_t (*xr)[kLatChunk], uint32_t lane, int (&po)[8], int (&ho)[8]) {
+  int p0[4], h0[4], p1[4], h1[4];
+  static_for<0, 4>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    p0[u] = d0[4 * u] + (d0[4 * u + 1] << 8);
+    h0[u] = d0[4 * u + 2] + (d0[4 * u + 3] << 8);
+    p1[u] = d1[4 * u] + (d1[4 * u + 1] << 8);
+    h1[u] = d1[4 * u + 2] + (d1[4 * u + 3] << 8);
+    swap32(p0[u], p1[u]);  // p0: own limb 2u, p1: own limb 2u + 1
+    swap32(h0[u], h1[u]);
+  });
+  static_for<0, 8>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    constexpr int q = 8 * MT + r, u = r >> 1;
+    if constexpr (q < kL) {
+      int p = (r & 1) ? p1[u] : p0[u];
+      if constexpr (q < kFoldF) p += (int)xr[q][lane];  // t_lo (signed Karatsuba limbs)
+      p += (int)cadd[q];
+      po[r] = p;
+      ho[r] = (r & 1) ? h1[u] : h0[u];
+    }
+  });
+}
+
+// The M-tiles MT0, MT0 + 4, MT0 + 8 (< 10) of one wave, their K-steps
+// interleaved (4-6 independent MFMA chains: alone on its SIMD a wave would
+// otherwise wait out each chain's latency), then -- once the block has finished
+// reading t (barrier 3, inside) -- the (p, h) pairs stored at rows 2q, 2q + 1.
+template <int MT0>
+__device__ __forceinline__ void lat_fold(const v4i* wl, cptr cadd, uint32_t (*xr)[kLatChunk], uint32_t lane) {
+  constexpr int NT = MT0 + 8 < kFoldMT ? 3 : 2;
+  v4i b0[kFoldKS], b1[kFoldKS];
+  static_for<0, kFoldKS>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<0, 4>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int jp = 8 * s + i, jq = 8 * s + 4 + i;
+      int p = 0, q = 0;  // t_hi arrives biased (kara_combine); padding K slots have zero weights
+      if constexpr (jp < kFoldNH) p = (int)xr[kFoldF + jp][lane];
+      if constexpr (jq < kFoldNH) q = (int)xr[kFoldF + jq][lane];
+      swap32(p, q);
+      b0[s][i] = p;
+      b1[s][i] = q;
+    });
+  });
+  v16i d0[NT], d1[NT];
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    d0[j] = v16i{};
+    d1[j] = v16i{};
+  });
+#if MOCHI_LAT_SEQ_TILES
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    static_for<0, kFoldKS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
+      d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
+      d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  });
+#else
+  static_for<0, kFoldKS>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<0, NT>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
+      d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
+      d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
+    });
+  });
+#endif
+  int po[3][8] = {}, ho[3][8] = {};
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    lat_assemble<MT0 + 4 * j>(d0[j], d1[j], cadd, xr, lane, po[j], ho[j]);
+  });
+  __syncthreads();  // barrier 3: every wave is done reading t
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    constexpr int mt = MT0 + 4 * j;
+    static_for<0, 8>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      constexpr int q = 8 * mt + r;
+      if constexpr (q < kL) {
+        xr[2 * q][lane] = (uint32_t)po[j][r];
+        xr[2 * q + 1][lane] = (uint32_t)ho[j][r];
+      }
+    });
+  });
+}
+
+// A 37-limb square's columns as independent 64-bit sums (no carry between
+// them, so the scheduler interleaves the chains -- a wave alone on its SIMD
+// would wait out each mad's latency along one chain), then one carry pass into
+// normalised limbs: out[0..2N].  a: 28- or 29-bit limbs (a column of the
+// 29-bit M sum stays < 19 * 2^59 < 2^64).
+template <int AO, int NOUT, int NA>
+__device__ __forceinline__ void lat_square(const uint32_t (&a)[NA], uint32_t (&out)[NOUT]) {
+  uint32_t d[kKH];
+#pragma unroll
+  for (int i = 0; i < kKH; i++) d[i] = a[AO + i] << 1;
+  uint64_t col[2 * kKH - 1];
+  static_for<0, 2 * kKH - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int lo = k - kKH + 1 > 0 ? k - kKH + 1 : 0;
+    constexpr int xhi = k > 0 ? (k - 1) / 2 : -1;
+    uint64_t acc = 0;
+    if constexpr ((k & 1) == 0) acc = (uint64_t)a[AO + (k >> 1)] * a[AO + (k >> 1)];
+    static_for<lo, xhi + 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      acc = mad64(d[i], a[AO + k - i], acc);
+    });
+    col[k] = acc;
+  });
+  uint64_t carry = 0;
+  static_for<0, NOUT>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (k < 2 * kKH - 1) {
+      const uint64_t v = col[k] + carry;
+      out[k] = (uint32_t)v & kLimbMask;
+      carry = v >> kLimbBits;
+    } else if constexpr (k == 2 * kKH - 1) {
+      out[k] = (uint32_t)carry & kLimbMask;
+    } else {
+      out[k] = (uint32_t)(carry >> kLimbBits);
+    }
+  });
+}
 
 __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
   __shared__ v4i w[kFoldImgBytes / 16];
-  __shared__ uint32_t xh[kL][kLatChunk];       // H = x_hi^2 (74 limbs)
-  __shared__ uint32_t xm[kL + 1][kLatChunk];   // M = (x_lo + x_hi)^2 (75 limbs)
-  __shared__ uint32_t xn[kL][kLatChunk];       // the folded x for waves 1 and 2
+  __shared__ uint32_t xr[kLatRows][kLatChunk];  // the exchange rows (lane-major: conflict-free)
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * kLatChunk;
   if (base >= a.n_slots) return;
@@ -260,59 +413,86 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
   const uint32_t g = slot < a.n_slots ? a.perm[slot] : 0xFFFFFFFFu;
   const bool active = g != 0xFFFFFFFFu;
   uint32_t x[kL];
-  if (wv < 3) {
+  {
     uint32_t wd[64];
     load_sig_words(a.sig, active ? g : g_lead, wd);  // inactive lanes shadow the lead grant (never stored)
     words_to_limbs(wd, x);
   }
   __syncthreads();
   const cptr c = as_const(a.fold[key].cadd);
+  const v4i* wl = w + lane;
 #pragma unroll 1
   for (int it = 0; it < 16; it++) {
-    if (it > 0 && (wv == 1 || wv == 2)) {  // the folded x of the last squaring
-#pragma unroll
-      for (int q = 0; q < kL; q++) x[q] = xn[q][lane];
-    }
     uint32_t lv[kL];
+#if MOCHI_LAT_RAW  // A/B: columns as independent sums + one carry pass (measured slower: 148 vs 138 us)
+    if (wv == 0) {  // L = x_lo^2, normalised, into registers
+      lat_square<0>(x, lv);
+    } else if (wv == 1) {  // H = x_hi^2 -> rows 0..73
+      uint32_t hv[kL];
+      lat_square<kKH>(x, hv);
+#pragma unroll
+      for (int k = 0; k < kL; k++) xr[k][lane] = hv[k];
+    } else if (wv == 2) {  // M = (x_lo + x_hi)^2 -> rows 74..148
+      uint32_t sx[kKH], mv[kL + 1];
+#pragma unroll
+      for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
+      lat_square<0>(sx, mv);
+#pragma unroll
+      for (int k = 0; k <= kL; k++) xr[kL + k][lane] = mv[k];
+    }
+#else
     if (wv == 0) {  // L = x_lo^2, normalised, into registers
       uint64_t carry = 0;
       static_for<0, kL>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         lv[k] = square_col<0, k>(x, carry);
       });
-    } else if (wv == 1) {  // H = x_hi^2
+    } else if (wv == 1) {  // H = x_hi^2 -> rows 0..73
       uint64_t carry = 0;
       static_for<0, kL>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        xh[k][lane] = square_col<kKH, k>(x, carry);
+        xr[k][lane] = square_col<kKH, k>(x, carry);
       });
-    } else if (wv == 2) {  // M = (x_lo + x_hi)^2
+    } else if (wv == 2) {  // M = (x_lo + x_hi)^2 -> rows 74..148
       uint32_t sx[kKH];
 #pragma unroll
       for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
       uint64_t carry = 0;
       static_for<0, kL + 1>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        xm[k][lane] = square_col<0, k>(sx, carry);
+        xr[kL + k][lane] = square_col<0, k>(sx, carry);
       });
     }
-    __syncthreads();
-    if (wv == 0) {
-      cptr ci = c;
-      asm volatile("" : "+s"(ci));
+#endif
+    __syncthreads();  // barrier 1: H and M written
+    if (wv == 0) {  // t = L + 2^(28*37) (M - L - H) + 2^(28*74) H (t_hi biased) -> rows 0..147
       uint32_t t[2 * kL];
 #pragma unroll
-      for (int k = 0; k <= kL; k++) t[kKH + k] = xm[k][lane];
+      for (int k = 0; k <= kL; k++) t[kKH + k] = xr[kL + k][lane];
       kara_combine(
           t, [&](auto kc, uint64_t&) { return lv[decltype(kc)::value]; },
-          [&](auto kc, uint64_t&) { return xh[decltype(kc)::value][lane]; });
-      fold_reduce<false, true>(t, x, w + lane, ci, nullptr);
-      if (it < 15) {
+          [&](auto kc, uint64_t&) { return xr[decltype(kc)::value][lane]; });
 #pragma unroll
-        for (int q = 0; q < kL; q++) xn[q][lane] = x[q];
+      for (int k = 0; k < 2 * kL; k++) xr[k][lane] = t[k];
+    }
+    __syncthreads();  // barrier 2: t written
+    cptr ci = c;
+    asm volatile("" : "+s"(ci));
+    if (wv == 0) lat_fold<0>(wl, ci, xr, lane);  // each contains barrier 3
+    else if (wv == 1) lat_fold<1>(wl, ci, xr, lane);
+    else if (wv == 2) lat_fold<2>(wl, ci, xr, lane);
+    else lat_fold<3>(wl, ci, xr, lane);
+    __syncthreads();  // barrier 4: every (p, h) pair written
+    if (wv < 3) {  // x' = sum_q (h_q 2^16 + p_q) 2^(28 q), normalised (fold_reduce's carry chain)
+      int64_t carry = 0;
+#pragma unroll
+      for (int q = 0; q < kL; q++) {
+        const int64_t v = mad_i64((int)xr[2 * q + 1][lane], 65536, mad_i64((int)xr[2 * q][lane], 1, carry));
+        x[q] = (uint32_t)v & kLimbMask;
+        carry = v >> kLimbBits;
       }
     }
-    __syncthreads();
+    __syncthreads();  // barrier 5: the pairs are read before the next H / M overwrite them
   }
   if (wv == 0 && active) {
 #pragma unroll
