@@ -65,7 +65,22 @@ struct PrepCertArgs {
   const uint32_t* same;  // [N] or null: an earlier grant of the certificate with the same bytes (the decoder's match)
   uint32_t n_certs;
   uint8_t* rare;         // [N]: 1 = prepped by k_grant_prep_rare (preset to 1: a grant outside every certificate too)
+  const uint8_t* expected;  // [n_certs][MOCHI_TXN_HASH_BYTES] or null: the leaders' hash checks (kHashChecked)
 };
+
+// A slot leader's hash_len word: its transactionHash compared with certificate
+// c's expected hash here, where the grant's bytes were just read (L2-warm), so
+// k_tally -- a serial stage with nothing to hide its memory round trips -- reads
+// one word for g0 instead of hash_off and 2 x 128 bytes.  Every grant reading
+// this distinct result through `lead` belongs to certificate c.
+__device__ __forceinline__ uint32_t leader_hash_word(const PrepArgs& a, const PrepCertArgs& p, uint32_t c,
+                                                     uint64_t og, const PrepOut& o) {
+  if (!p.expected || !(o.flags & MOCHI_GRANT_PARSED)) return hash_len_word(o);
+  static_assert(MOCHI_TXN_HASH_BYTES == 128, "bytes128_equal");
+  const bool eq = o.hash_len == MOCHI_TXN_HASH_BYTES &&
+                  bytes128_equal(a.blob + og + o.hash_rel, p.expected + (size_t)c * MOCHI_TXN_HASH_BYTES);
+  return kHashChecked | (eq ? kHashEq : 0u);
+}
 
 // The block's first-slot per-grant outputs go out through LDS: each lane puts
 // its leader's timestamp and flags in `lo` and marks the leader and its
@@ -145,7 +160,7 @@ __global__ __launch_bounds__(256) MOCHI_PREP_ATTR void k_grant_prep_cert(const P
       const uint32_t lg = a.glen[g];
       grant_prep_bytes(a.blob + og, lg, o);
       const uint32_t d = leaders == 1 ? c : a.d_base + g;
-      grant_prep_store_dist(a, d, og, o);
+      grant_prep_store_dist(a, d, og, o, leader_hash_word(a, p, c, og, o));
       if (via_lds) {
         PrepOutLds& e = lo[threadIdx.x];
         e.ts_lo = (uint32_t)o.ts;
@@ -589,6 +604,35 @@ __device__ __noinline__ bool grant_bound_at(const uint8_t* gp, uint32_t glen, co
   return hash_matches(gp, ho, hl, expected);
 }
 
+// g0's transactionHash == expected, g0's distinct result at d: the leader's
+// check (kHashChecked), else the bytes.  kLean (the launch with
+// k_grant_prep_cert's checks, no MOCHI_Q_BIND) compares a grant prepped on its
+// own -- rare -- 16 bytes at a time; the two-window compare (the other launches:
+// the small-batch sequence, whose per-grant prep checks nothing, and the bind
+// mode, whose Grant parse is a call) or a call would set k_tally's register count:
+// 118 VGPRs and 4 waves per SIMD against 49 and 8 without (the tally waits on
+// memory, so its occupancy is its speed).
+__device__ __forceinline__ bool hash_matches_lean(const uint8_t* __restrict__ gp, const uint8_t* __restrict__ e) {
+  uint32_t diff = 0;
+#pragma unroll 1
+  for (uint32_t pos = 0; pos < MOCHI_TXN_HASH_BYTES; pos += 16) {
+    uint32_t wa[4], wb[4];
+    window16(gp, MOCHI_TXN_HASH_BYTES, pos, wa);
+    window16(e, MOCHI_TXN_HASH_BYTES, pos, wb);
+#pragma unroll
+    for (int t = 0; t < 4; t++) diff |= wa[t] ^ wb[t];
+  }
+  return diff == 0;
+}
+
+template <bool kLean>
+__device__ __forceinline__ bool g0_hash_matches(const TallyArgs& a, uint32_t d, const uint8_t* expected) {
+  const uint32_t hl = a.hash_len[d];
+  if (hl & kHashChecked) return (hl & kHashEq) != 0;
+  if (!kLean) return hash_matches(a.blob, a.hash_off[d], hl, expected);
+  return hl == MOCHI_TXN_HASH_BYTES && hash_matches_lean(a.blob + a.hash_off[d], expected);
+}
+
 __device__ __forceinline__ bool grant_bound(const TallyArgs& a, uint32_t g, uint32_t o, const uint8_t* expected) {
   if (!a.op_key_off || !a.op_key_len) return false;
   return grant_bound_at(a.blob + a.grant_off[g], a.grant_len[g], a.blob + a.op_key_off[o], a.op_key_len[o], expected);
@@ -598,6 +642,7 @@ __device__ __forceinline__ bool grant_bound(const TallyArgs& a, uint32_t g, uint
 // signature verified -- invalid => absent, InMemoryDataStore.java:622-624 --
 // and an op names its slot); MOCHI_Q_BIND / MOCHI_Q_DISTINCT_SIGNERS exclude
 // more.  first_op[] is not kept per lane: the op naming slot s is found by scan.
+template <bool kLean>
 __device__ bool counts(const TallyArgs& a, uint32_t g, uint32_t g_lo, uint32_t o_lo, uint32_t o_hi,
                        const uint8_t* expected) {
   if (!(a.flags[g] & MOCHI_GRANT_SIG_OK)) return false;
@@ -611,7 +656,7 @@ __device__ bool counts(const TallyArgs& a, uint32_t g, uint32_t g_lo, uint32_t o
       break;
     }
   if (fo == 0xFFFFFFFFu) return false;  // no op looks this key up
-  const bool bind = a.quorum_mode & MOCHI_Q_BIND;
+  const bool bind = !kLean && (a.quorum_mode & MOCHI_Q_BIND);
   if (bind && !grant_bound(a, g, fo, expected)) return false;
   if (a.quorum_mode & MOCHI_Q_DISTINCT_SIGNERS) {
     // the first grant of (slot, signer) that passes the other checks counts
@@ -686,6 +731,7 @@ __device__ bool incoming_cert_ok(const TallyArgs& a, uint32_t c, uint32_t g_lo, 
 #else
 #define MOCHI_TALLY_ATTR
 #endif
+template <bool kLean>
 __global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs a) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t reason = MOCHI_ACCEPT, fail_op = 0xFF;
@@ -706,7 +752,7 @@ __global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs 
         bool seen = false;
         int64_t ts0 = 0;
         for (uint32_t g = g_lo; g < g_hi; g++) {
-          if (a.grant_key[g] != s || !counts(a, g, g_lo, o_lo, o_hi, expected)) continue;
+          if (a.grant_key[g] != s || !counts<kLean>(a, g, g_lo, o_lo, o_hi, expected)) continue;
           if (!seen) {
             seen = true;
             ts0 = a.ts[g];
@@ -735,7 +781,7 @@ __global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs 
         }
         uint32_t valid = 0, first = 0xFFFFFFFFu;
         for (uint32_t g = g_lo; g < g_hi; g++) {
-          if (a.grant_key[g] != s || !counts(a, g, g_lo, o_lo, o_hi, expected)) continue;
+          if (a.grant_key[g] != s || !counts<kLean>(a, g, g_lo, o_lo, o_hi, expected)) continue;
           if (first == 0xFFFFFFFFu) first = g;
           valid++;
         }
@@ -743,8 +789,7 @@ __global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs 
         uint32_t why = MOCHI_ACCEPT;
         if (first == 0xFFFFFFFFu) why = MOCHI_REJECT_NO_GRANT;                                      // :588
         else if (!(a.strict_gt ? cnt > a.majority : cnt >= a.majority)) why = MOCHI_REJECT_BELOW_QUORUM;  // :590
-        else if (!hash_matches(a.blob, a.hash_off[a.lead ? a.lead[first] : first],
-                               a.hash_len[a.lead ? a.lead[first] : first], expected))
+        else if (!g0_hash_matches<kLean>(a, a.lead ? a.lead[first] : first, expected))
           why = MOCHI_REJECT_HASH_MISMATCH;                                                       // :591,605-607
         else if (!(fl & MOCHI_OP_HAS_SVOC)) why = MOCHI_REJECT_NO_SVOC;                           // :592-593
         else {
@@ -775,7 +820,7 @@ __global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs 
         const uint32_t j = o - o_lo, s = a.op_key[o];
         uint32_t first = 0xFFFFFFFFu;
         for (uint32_t g = g_lo; g < g_hi && first == 0xFFFFFFFFu; g++)
-          if (a.grant_key[g] == s && counts(a, g, g_lo, o_lo, o_hi, expected)) first = g;
+          if (a.grant_key[g] == s && counts<kLean>(a, g, g_lo, o_lo, o_hi, expected)) first = g;
         uint32_t d = MOCHI_OPD_SKIPPED;
         if ((applied >> j) & 1) d = MOCHI_OPD_APPLY;
         else if ((read >> j) & 1) d = MOCHI_OPD_READ;
@@ -832,6 +877,15 @@ static bool dedup_off() {
     return e && e[0] == '1';
   }();
   return off;
+}
+
+// MOCHI_NO_HASH_PRECHECK=1 (A/B): k_tally compares every g0 hash itself
+static bool hash_precheck() {
+  static const bool on = [] {
+    const char* e = getenv("MOCHI_NO_HASH_PRECHECK");
+    return !(e && e[0] == '1');
+  }();
+  return on;
 }
 
 // MOCHI_NO_SMALL=1 (A/B): small batches take the large-batch launch sequence
@@ -914,7 +968,8 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     mark(kStagePrep, false, ps);
     if (prep) {
       if (dedup) {
-        const PrepCertArgs pc{a.grant_key, a.cert_grant_off, a.grant_same, C, a.rare};
+        const PrepCertArgs pc{a.grant_key, a.cert_grant_off, a.grant_same, C, a.rare,
+                              hash_precheck() ? a.expected_hash : nullptr};
         hipError_t e = hipMemsetAsync(a.rare, 1, N, ps);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_grant_prep_cert, dim3(cdiv(C, 256)), dim3(256), 0, ps, pa, pc);
@@ -1005,7 +1060,11 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     t.op_g0 = a.op_g0;
     t.op_ts = a.op_ts;
     t.op_out_off = a.op_out_off;
-    hipLaunchKernelGGL(k_tally, dim3(cdiv(C, 256)), dim3(256), 0, st, t);
+    // lean: every slot leader's hash checked in k_grant_prep_cert, no bind mode
+    if (dedup && hash_precheck() && !(a.quorum_mode & MOCHI_Q_BIND))
+      hipLaunchKernelGGL(k_tally<true>, dim3(cdiv(C, 256)), dim3(256), 0, st, t);
+    else
+      hipLaunchKernelGGL(k_tally<false>, dim3(cdiv(C, 256)), dim3(256), 0, st, t);
   }
   mark(kStageTally, true, st);
   return hipGetLastError();

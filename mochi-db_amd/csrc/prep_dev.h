@@ -158,16 +158,31 @@ __device__ __forceinline__ void grant_prep_bytes(const uint8_t* p, uint32_t l, P
   sha256(p, l, o.h);
   o.ts = ok ? ts : 0;
   o.hash_rel = hoff;
-  o.hash_len = ok ? hlen : 0xFFFFFFFFu;
+  o.hash_len = ok ? hlen : 0u;  // unparsed: k_tally rejects the certificate before its hash check
   o.flags = ok ? MOCHI_GRANT_PARSED : 0;
 }
 
+// hash_len[d] with kHashChecked set: k_grant_prep_cert already compared the
+// transactionHash with its certificate's expected hash (kHashEq = equal), so
+// k_tally reads this word instead of both hashes.  A plain length is kept below
+// kHashEq (a length that large is never MOCHI_TXN_HASH_BYTES: same verdict).
+constexpr uint32_t kHashChecked = 0x80000000u, kHashEq = 0x40000000u;
+
+__device__ __forceinline__ uint32_t hash_len_word(const PrepOut& o) {
+  return o.hash_len < kHashEq ? o.hash_len : kHashEq - 1u;
+}
+
 // The distinct result d of grant bytes at offset `goff` (hash_off is absolute).
-__device__ __forceinline__ void grant_prep_store_dist(const PrepArgs& a, uint32_t d, uint64_t goff, const PrepOut& o) {
+__device__ __forceinline__ void grant_prep_store_dist(const PrepArgs& a, uint32_t d, uint64_t goff, const PrepOut& o,
+                                                      uint32_t hash_word) {
 #pragma unroll
   for (int q = 0; q < 8; q++) a.digest[(size_t)q * a.nd + d] = o.h[q];
   a.hash_off[d] = goff + o.hash_rel;
-  a.hash_len[d] = o.hash_len;
+  a.hash_len[d] = hash_word;
+}
+
+__device__ __forceinline__ void grant_prep_store_dist(const PrepArgs& a, uint32_t d, uint64_t goff, const PrepOut& o) {
+  grant_prep_store_dist(a, d, goff, o, hash_len_word(o));
 }
 
 // Grant g's own outputs, its result at distinct index d.
@@ -238,6 +253,21 @@ __device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t 
     if (diff) return false;
   }
   return true;
+}
+
+// 128 bytes at a and at b (any alignment) equal: all four 64-byte windows
+// issued before the compare -- one memory round trip, not bytes_equal's one per
+// window (callers that have the registers: k_grant_prep_cert after its SHA-256)
+__device__ __forceinline__ bool bytes128_equal(const uint8_t* a, const uint8_t* b) {
+  uint32_t a0[16], a1[16], b0[16], b1[16];
+  window64(a, 128, 0, a0);
+  window64(a, 128, 64, a1);
+  window64(b, 128, 0, b0);
+  window64(b, 128, 64, b1);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int t = 0; t < 16; t++) diff |= (a0[t] ^ b0[t]) | (a1[t] ^ b1[t]);
+  return diff == 0;
 }
 
 }  // namespace mochi

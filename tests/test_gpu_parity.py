@@ -151,18 +151,24 @@ def test_rsa_golden_vectors_gpu(golden_dir):
     ver.close()
 
 
+@pytest.mark.parametrize("seq", ["small", "dedup"])
 @pytest.mark.parametrize("explicit_mg", [True, False])
 @pytest.mark.parametrize("key", sorted(grouped_cases().keys()))
-def test_cert_branch_cases_gpu(key, explicit_mg):
+def test_cert_branch_cases_gpu(key, explicit_mg, seq):
     """Every branch fixture on the device: GPU == oracle array for array (grant flags,
     timestamps, accept bits, reasons, failing ops, per-op decisions / g0 / ts) and
-    both == the hand-derived expectations."""
+    both == the hand-derived expectations.  `seq`: the small-batch launch sequence
+    (these batches' default) and the large-batch one (certificate-level dedup, slot
+    leaders' hashes checked in k_grant_prep_cert, the lean k_tally outside
+    MOCHI_Q_BIND)."""
     R, strict, qm = key
     cases = grouped_cases(explicit_mg).get(key)
     if not cases:
         pytest.skip("every case of this group needs explicit MultiGrants")
     batch, ex = build_case_batch(cases, W.load_keys(R), explicit_mg)
     ver = mh.Verifier(moduli_for(R), 0)
+    if seq == "dedup":
+        ver.set_small_batch(0)
     g = ver.verify(batch, R, bool(strict), quorum_mode=qm)
     o = O.verify_batch(moduli_for(R), batch, R, bool(strict), 4, quorum_mode=qm)
     assert_same(g, o, str(key))
@@ -468,11 +474,12 @@ def _sign_cached(pem, gb):
     return _SIG_CACHE[key]
 
 
-def _dedup_batch(pems, certs, shared_first=False):
+def _dedup_batch(pems, certs, shared_first=False, bad_sig=()):
     """certs: list of lists of (grant bytes, signer, key slot); every grant its own copy
     in the blob at a varying alignment (the byte compares of k_grant_prep_cert /
     k_grant_match), or -- with shared_first -- grants equal to the certificate's first
-    one pointing at its bytes (the SoA layout's offset shortcut)."""
+    one pointing at its bytes (the SoA layout's offset shortcut).  bad_sig: (cert,
+    grant) pairs whose signature gets one byte flipped."""
     blob = bytearray(b"\x07")
     offs, lens, sigs, signer, gkey, cgo = [], [], [], [], [], [0]
     cop, opk = [0], []
@@ -488,7 +495,10 @@ def _dedup_batch(pems, certs, shared_first=False):
                 if first is None:
                     first = (gb, offs[-1])
             lens.append(len(gb))
-            sigs.append(_sign_cached(pems[s], gb))
+            sg = _sign_cached(pems[s], gb)
+            if (ci, gi) in bad_sig:
+                sg = sg[:100] + bytes([sg[100] ^ 0x40]) + sg[101:]
+            sigs.append(sg)
             signer.append(s)
             gkey.append(k)
         cgo.append(len(offs))
@@ -581,6 +591,40 @@ def test_grant_dedup_block_over_lds_and_third_slot(pool4, dedup_path, shared_fir
         o = O.verify_batch(pool4.moduli, b, 4, strict, 4)
         assert_same(got, o, f"strict={strict}")
     assert (got.cert_reason == mh.REJECT_TS_MISMATCH).any() and (got.cert_reason == mh.ACCEPT).any()
+
+
+@pytest.mark.parametrize("shared_first", [False, True])
+def test_g0_hash_after_an_invalid_leader(pool4, dedup_path, shared_first):
+    """g0 is not always its slot's first grant: with the first grant's signature
+    invalid (absent, InMemoryDataStore.java:622-624) g0 is the next counted grant.
+    When that grant differs from the first in its bytes its result is its own
+    (k_grant_prep_rare), with no hash check from k_grant_prep_cert, and the lean
+    k_tally compares its transactionHash itself, 16 bytes at a time -- equal (accept)
+    and one byte off (REJECT_HASH_MISMATCH), at every alignment of the copy."""
+    pems = W.load_keys(4)
+    th = W.txn_hash_hex(9)
+    oth = th[:-1] + ("0" if th[-1] != "0" else "1")
+    base = W.encode_grant("DEMO_KEY_G0", 1000, th)
+    longer = base + b"\x30\x01"  # same timestamp and hash, other bytes
+    hmis = W.encode_grant("DEMO_KEY_G0", 1000, oth)
+    hmis_longer = hmis + b"\x30\x01"
+    variants = {"g0_ok": [base, longer, longer, longer], "g0_bad": [base, hmis, hmis, hmis],
+                "g0_bad_tail": [base, hmis_longer, hmis_longer, longer],
+                "g0_ok_lead_ok": [base, longer, base, base]}
+    certs, bad = [], set()
+    for rep in range(24):
+        for name, gs in variants.items():
+            if name != "g0_ok_lead_ok":
+                bad.add((len(certs), 0))
+            certs.append([(gb, r, 0) for r, gb in enumerate(gs)])
+    b = _dedup_batch(pems, certs, shared_first, bad_sig=bad)
+    for strict in (True, False):
+        got = dedup_path.verify(b, 4, strict)
+        o = O.verify_batch(pool4.moduli, b, 4, strict, 4)
+        assert_same(got, o, f"strict={strict}")
+    reasons = {k: int(got.cert_reason[i]) for i, k in enumerate(variants)}
+    assert reasons["g0_ok"] == mh.ACCEPT and reasons["g0_ok_lead_ok"] == mh.ACCEPT
+    assert reasons["g0_bad"] == mh.REJECT_HASH_MISMATCH and reasons["g0_bad_tail"] == mh.REJECT_HASH_MISMATCH
 
 
 def test_grant_dedup_large_certificate(pool4, dedup_path):
