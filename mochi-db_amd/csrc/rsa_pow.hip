@@ -60,6 +60,9 @@
 #ifndef MOCHI_LAT_SEQ_TILES
 #define MOCHI_LAT_SEQ_TILES 0  // A/B: k_rsa_pow_lat's M-tiles one after the other
 #endif
+#ifndef MOCHI_LAT_ONE_TILE
+#define MOCHI_LAT_ONE_TILE 1  // A/B (0): k_rsa_pow_lat always folds both N-tiles
+#endif
 #ifndef MOCHI_POW_NEXT_AHEAD
 #define MOCHI_POW_NEXT_AHEAD 1  // the next group's index fetched one group ahead (below)
 #endif
@@ -159,6 +162,9 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
       continue;
     }
     const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)a.signer[g_lead]);
+  // a signature among slots 32-63 (else the fold's second N-tile is skipped)
+  const bool two = MOCHI_LAT_ONE_TILE == 0 ||
+                   __builtin_amdgcn_readfirstlane(base + 32 < a.n_slots && a.perm[base + 32] != 0xFFFFFFFFu);
     if (key != cur_key) {
       __syncthreads();  // the old image is no longer read
       const v4i* src = (const v4i*)a.fold[key].img;
@@ -292,7 +298,11 @@ __device__ __forceinline__ void lat_assemble(const v16i& d0, const v16i& d1, cpt
 // interleaved (4-6 independent MFMA chains: alone on its SIMD a wave would
 // otherwise wait out each chain's latency), then -- once the block has finished
 // reading t (barrier 3, inside) -- the (p, h) pairs stored at rows 2q, 2q + 1.
-template <int MT0>
+// !kTwo: slots 32-63 of the chunk are empty (a bucket fills from its start), so
+// the second N-tile (signatures 32-63) is skipped -- half the MFMAs; lanes
+// 32-63 then carry garbage, and they are never stored (a batcher flush of a few
+// messages has 1-2 grants per signer bucket).
+template <int MT0, bool kTwo>
 __device__ __forceinline__ void lat_fold(const v4i* wl, cptr cadd, uint32_t (*xr)[kLatChunk], uint32_t lane) {
   constexpr int NT = MT0 + 8 < kFoldMT ? 3 : 2;
   v4i b0[kFoldKS], b1[kFoldKS];
@@ -322,7 +332,7 @@ __device__ __forceinline__ void lat_fold(const v4i* wl, cptr cadd, uint32_t (*xr
       constexpr int s = decltype(sc)::value;
       const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
       d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
-      d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
+      if constexpr (kTwo) d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     });
   });
@@ -333,7 +343,7 @@ __device__ __forceinline__ void lat_fold(const v4i* wl, cptr cadd, uint32_t (*xr
       constexpr int j = decltype(jc)::value;
       const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
       d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
-      d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
+      if constexpr (kTwo) d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
     });
   });
 #endif
@@ -405,6 +415,9 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
   const uint32_t g_lead = __builtin_amdgcn_readfirstlane(a.perm[base]);
   if (g_lead == 0xFFFFFFFFu) return;
   const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)a.signer[g_lead]);
+  // a signature among slots 32-63 (else the fold's second N-tile is skipped)
+  const bool two = MOCHI_LAT_ONE_TILE == 0 ||
+                   __builtin_amdgcn_readfirstlane(base + 32 < a.n_slots && a.perm[base + 32] != 0xFFFFFFFFu);
   {
     const v4i* src = (const v4i*)a.fold[key].img;
     for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
@@ -478,10 +491,17 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
     __syncthreads();  // barrier 2: t written
     cptr ci = c;
     asm volatile("" : "+s"(ci));
-    if (wv == 0) lat_fold<0>(wl, ci, xr, lane);  // each contains barrier 3
-    else if (wv == 1) lat_fold<1>(wl, ci, xr, lane);
-    else if (wv == 2) lat_fold<2>(wl, ci, xr, lane);
-    else lat_fold<3>(wl, ci, xr, lane);
+    if (two) {  // each contains barrier 3
+      if (wv == 0) lat_fold<0, true>(wl, ci, xr, lane);
+      else if (wv == 1) lat_fold<1, true>(wl, ci, xr, lane);
+      else if (wv == 2) lat_fold<2, true>(wl, ci, xr, lane);
+      else lat_fold<3, true>(wl, ci, xr, lane);
+    } else {
+      if (wv == 0) lat_fold<0, false>(wl, ci, xr, lane);
+      else if (wv == 1) lat_fold<1, false>(wl, ci, xr, lane);
+      else if (wv == 2) lat_fold<2, false>(wl, ci, xr, lane);
+      else lat_fold<3, false>(wl, ci, xr, lane);
+    }
     __syncthreads();  // barrier 4: every (p, h) pair written
     if (wv < 3) {  // x' = sum_q (h_q 2^16 + p_q) 2^(28 q), normalised (fold_reduce's carry chain)
       int64_t carry = 0;

@@ -1,6 +1,6 @@
 # A/B of k_rsa_pow_lat variants (in-tree lib, and each of $LIBS) on single small
 # mochi_verify_write2 calls, alternated, then a kernel trace of each.
-LIBS="mochi-db_amd/libmochi_hip_seq.so mochi-db_amd/libmochi_hip_raw.so"
+LIBS="${LIBS:-mochi-db_amd/libmochi_hip_seq.so mochi-db_amd/libmochi_hip_raw.so}"
 for i in 1 2; do
   for v in A $LIBS; do
     if [ $v = A ]; then L=""; t=A; else L="$PWD/$v"; t=$(basename $v .so); fi
