@@ -136,6 +136,125 @@ __device__ __forceinline__ void fold_reduce(const uint32_t (&t)[2 * kL], uint32_
   });
 }
 
+// ---------------------------------------------------------------------------
+// The fold split over a block's four waves for the latency kernels of small
+// batches (k_rsa_pow_lat, k_rsa_final_lat): every wave holds the same 64 slots;
+// t sits in the LDS exchange rows xr (lane-major), wave w folds M-tiles w, w+4,
+// w+8 and writes each output limb's two int32 halves (p, h) back into the rows;
+// the limb arithmetic is fold_reduce's, split by tile (bit-exact with it).
+// ---------------------------------------------------------------------------
+#ifndef MOCHI_LAT_SEQ_TILES
+#define MOCHI_LAT_SEQ_TILES 0  // A/B: the latency kernels' M-tiles one after the other
+#endif
+constexpr uint32_t kLatChunk = 64;
+constexpr int kLatRows = 2 * kL + 1;  // 149 rows: H + M, then t (148), then the (p, h) pairs (148)
+
+// The (p, h) halves of output limb q of an M-tile from its accumulators (the
+// MFMA layout: half h of the wave holds limb 2u + h of both N-tiles'
+// signatures; one swap per half turns them into this lane's own limbs)
+template <int MT, bool SUB_H>
+__device__ __forceinline__ void lat_assemble(const v16i& d0, const v16i& d1, cptr cadd,
+                                             const uint32_t (*xr)[kLatChunk], uint32_t lane, const uint32_t (&hl)[kHL],
+                                             int (&po)[8], int (&ho)[8]) {
+  int p0[4], h0[4], p1[4], h1[4];
+  static_for<0, 4>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    p0[u] = d0[4 * u] + (d0[4 * u + 1] << 8);
+    h0[u] = d0[4 * u + 2] + (d0[4 * u + 3] << 8);
+    p1[u] = d1[4 * u] + (d1[4 * u + 1] << 8);
+    h1[u] = d1[4 * u + 2] + (d1[4 * u + 3] << 8);
+    swap32(p0[u], p1[u]);  // p0: own limb 2u, p1: own limb 2u + 1
+    swap32(h0[u], h1[u]);
+  });
+  static_for<0, 8>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    constexpr int q = 8 * MT + r, u = r >> 1;
+    if constexpr (q < kL) {
+      int p = (r & 1) ? p1[u] : p0[u];
+      if constexpr (q < kFoldF) p += (int)xr[q][lane];  // t_lo (signed Karatsuba limbs)
+      p += (int)cadd[q];
+      if constexpr (SUB_H && q < kHL) p -= (int)hl[q];  // k_rsa_final_lat: - H, as fold_reduce<true>
+      po[r] = p;
+      ho[r] = (r & 1) ? h1[u] : h0[u];
+    }
+  });
+}
+
+// The M-tiles MT0, MT0 + 4, MT0 + 8 (< 10) of one wave, their K-steps
+// interleaved (4-6 independent MFMA chains: alone on its SIMD a wave would
+// otherwise wait out each chain's latency), then -- once the block has finished
+// reading t (barrier 3, inside) -- the (p, h) pairs stored at rows 2q, 2q + 1.
+// !kTwo: slots 32-63 of the chunk are empty (a bucket fills from its start), so
+// the second N-tile (signatures 32-63) is skipped -- half the MFMAs; lanes
+// 32-63 then carry garbage, and they are never stored (a batcher flush of a few
+// messages has 1-2 grants per signer bucket).
+template <int MT0, bool kTwo, bool SUB_H = false>
+__device__ __forceinline__ void lat_fold(const v4i* wl, cptr cadd, uint32_t (*xr)[kLatChunk], uint32_t lane,
+                                         const uint32_t (&hl)[kHL]) {
+  constexpr int NT = MT0 + 8 < kFoldMT ? 3 : 2;
+  v4i b0[kFoldKS], b1[kFoldKS];
+  static_for<0, kFoldKS>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<0, 4>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int jp = 8 * s + i, jq = 8 * s + 4 + i;
+      int p = 0, q = 0;  // t_hi arrives biased (kara_combine); padding K slots have zero weights
+      if constexpr (jp < kFoldNH) p = (int)xr[kFoldF + jp][lane];
+      if constexpr (jq < kFoldNH) q = (int)xr[kFoldF + jq][lane];
+      swap32(p, q);
+      b0[s][i] = p;
+      b1[s][i] = q;
+    });
+  });
+  v16i d0[NT], d1[NT];
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    d0[j] = v16i{};
+    d1[j] = v16i{};
+  });
+#if MOCHI_LAT_SEQ_TILES
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    static_for<0, kFoldKS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
+      d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
+      if constexpr (kTwo) d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  });
+#else
+  static_for<0, kFoldKS>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<0, NT>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
+      d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
+      if constexpr (kTwo) d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
+    });
+  });
+#endif
+  int po[3][8] = {}, ho[3][8] = {};
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    lat_assemble<MT0 + 4 * j, SUB_H>(d0[j], d1[j], cadd, xr, lane, hl, po[j], ho[j]);
+  });
+  __syncthreads();  // barrier 3: every wave is done reading t
+  static_for<0, NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    constexpr int mt = MT0 + 4 * j;
+    static_for<0, 8>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      constexpr int q = 8 * mt + r;
+      if constexpr (q < kL) {
+        xr[2 * q][lane] = (uint32_t)po[j][r];
+        xr[2 * q + 1][lane] = (uint32_t)ho[j][r];
+      }
+    });
+  });
+}
+
+
 // Persistent walk over 512-slot groups of one signer (buckets are 512-aligned):
 // block b takes a contiguous range of groups; fn(base, key) runs per non-empty
 // group after the signer's fold image is staged in `w` (restaged only when the

@@ -95,7 +95,9 @@ hipError_t launch_withhold(const uint8_t* flags, uint32_t n, uint8_t* sig, uint3
 hipError_t launch_pack_bits(const uint8_t* flags, uint32_t n, uint8_t mask, uint32_t* bits, hipStream_t stream);
 // latency: the small-batch form (k_rsa_pow_lat: one signature chain spread over three SIMDs)
 void launch_rsa_pow(const LaunchArgs& a, hipStream_t stream, bool latency = false);
-void launch_rsa_final(const LaunchArgs& a, const uint32_t* lead, uint32_t n_dist, hipStream_t stream);
+// latency: a small batch -- k_rsa_final_lat, one 4-wave block per 64-slot chunk
+void launch_rsa_final(const LaunchArgs& a, const uint32_t* lead, uint32_t n_dist, hipStream_t stream,
+                      bool latency = false);
 void launch_rsa_raw(const LaunchArgs& a, hipStream_t stream);  // dbg_y path (mochi_rsa_public_op)
 
 }  // namespace mochi

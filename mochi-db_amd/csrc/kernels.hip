@@ -1020,7 +1020,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   }
   mark(kStageFinal, false, st);
   if (N) {
-    launch_rsa_final(a, lead, nd, st);
+    launch_rsa_final(a, lead, nd, st, small);
     if (a.grant_valid_bits)
       hipLaunchKernelGGL(k_pack_bits, dim3(cdiv(N, 256)), dim3(256), 0, st, a.flags, N, (uint8_t)MOCHI_GRANT_SIG_OK,
                          a.grant_valid_bits);

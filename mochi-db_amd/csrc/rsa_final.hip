@@ -28,6 +28,8 @@
 #include "fold_dev.h"
 #include "rsa_common.h"
 
+#include <cstdlib>
+
 // A/B: groups from a device counter (fold_dev.h for_groups), as k_rsa_pow's --
 // measured 1.6 % slower here (5.29-5.31 vs 5.21 ms), so the contiguous ranges stay
 #ifndef MOCHI_FINAL_DYN
@@ -243,11 +245,183 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final(const uint32_t* __restrict
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// k_rsa_final_lat — k_rsa_final for a SMALL batch (a batcher flush: one or two
+// grants per signer bucket), where one lone wave per 64-slot group spends
+// ~22k cycles on the product and ~12k on the fold.  As in k_rsa_pow_lat, a block
+// of 4 waves owns one 64-slot chunk and splits the work over the CU's SIMDs:
+//   t = z s:  wave 0 L = z_lo s_lo (registers), wave 1 H = z_hi s_hi, wave 2
+//             M = (z_lo + z_hi)(s_lo + s_hi) (both to LDS) at once; wave 0
+//             combines them (kara_combine) into t in LDS;
+//   fold:     wave w folds M-tiles w, w+4, w+8 (fold_dev.h lat_fold, with the
+//             final's constant cnc and the digest H subtracted, as
+//             fold_reduce<true, true>); the second N-tile only when slots
+//             32-63 hold a grant;
+//   then wave 0 runs the carry chain, the Montgomery step and the compare with
+//             n, and stores the flags -- the arithmetic of final_slot, so the
+//             verdicts are bit-exact with k_rsa_final (every small batch of the
+//             parity tests runs through it).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 1) void k_rsa_final_lat(const uint32_t* __restrict__ perm, uint32_t n_slots,
+                                                           const uint8_t* __restrict__ sig,
+                                                           const uint16_t* __restrict__ signer,
+                                                           const KeyEntry* __restrict__ keys,
+                                                           const FoldKey* __restrict__ fold,
+                                                           const uint32_t* __restrict__ zin,
+                                                           const uint32_t* __restrict__ digest,
+                                                           const uint32_t* __restrict__ lead, uint32_t n_dist,
+                                                           uint8_t* __restrict__ flags) {
+  __shared__ v4i w[kFoldImgBytes / 16];
+  __shared__ uint32_t xr[kLatRows][kLatChunk];  // the exchange rows (lane-major)
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * kLatChunk;
+  if (base >= n_slots) return;
+  // buckets are filled from their start: a chunk whose first slot is empty is all padding
+  const uint32_t g_lead = __builtin_amdgcn_readfirstlane(perm[base]);
+  if (g_lead == 0xFFFFFFFFu) return;
+  const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)signer[g_lead]);
+  {
+    const v4i* src = (const v4i*)fold[key].img;
+    for (uint32_t i = threadIdx.x; i < kFoldImgBytes / 16; i += blockDim.x) w[i] = src[i];
+  }
+  const bool two = __builtin_amdgcn_readfirstlane(base + 32 < n_slots && perm[base + 32] != 0xFFFFFFFFu);
+  const uint32_t slot = base + lane;
+  const uint32_t g = slot < n_slots ? perm[slot] : 0xFFFFFFFFu;
+  const bool active = g != 0xFFFFFFFFu;
+  const uint32_t gg = active ? g : g_lead;  // inactive lanes shadow the lead grant (never stored)
+  const uint32_t fl = flags[gg];  // the parse flags (grant prep), OR'd with SIG_OK at the end
+  uint32_t z[kL], sv[kL];
+#pragma unroll
+  for (int j = 0; j < kL; j++) z[j] = zin[(size_t)j * n_slots + (slot < n_slots ? slot : base)];
+  {
+    uint32_t wd[64];
+    load_sig_words(sig, gg, wd);
+    words_to_limbs(wd, sv);
+  }
+  __syncthreads();  // the image is staged
+  uint32_t lv[kL];
+  if (wv == 0) {  // L = z_lo s_lo, normalised, into registers
+    uint64_t carry = 0;
+    static_for<0, kL>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      lv[k] = product_col<0, 0, k>(z, sv, carry);
+    });
+  } else if (wv == 1) {  // H = z_hi s_hi -> rows 0..73
+    uint64_t carry = 0;
+    static_for<0, kL>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      xr[k][lane] = product_col<kKH, kKH, k>(z, sv, carry);
+    });
+  } else if (wv == 2) {  // M = (z_lo + z_hi)(s_lo + s_hi) -> rows 74..148
+    uint32_t sz[kKH], ss[kKH];
+#pragma unroll
+    for (int i = 0; i < kKH; i++) {
+      sz[i] = z[i] + z[kKH + i];
+      ss[i] = sv[i] + sv[kKH + i];
+    }
+    uint64_t carry = 0;
+    static_for<0, kL + 1>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      xr[kL + k][lane] = product_col<0, 0, k>(sz, ss, carry);
+    });
+  }
+  __syncthreads();  // barrier 1: H and M written
+  if (wv == 0) {  // t = L + 2^(28*37) (M - L - H) + 2^(28*74) H (t_hi biased) -> rows 0..147
+    uint32_t t[2 * kL];
+#pragma unroll
+    for (int k = 0; k <= kL; k++) t[kKH + k] = xr[kL + k][lane];
+    kara_combine(
+        t, [&](auto kc, uint64_t&) { return lv[decltype(kc)::value]; },
+        [&](auto kc, uint64_t&) { return xr[decltype(kc)::value][lane]; });
+#pragma unroll
+    for (int k = 0; k < 2 * kL; k++) xr[k][lane] = t[k];
+  }
+  // the digest H as 10 limbs (digest word 0 = most significant 4 bytes of H)
+  uint32_t hl[kHL];
+  {
+    const uint32_t d = lead ? lead[gg] : gg;
+    uint32_t hw[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) hw[i] = digest[(size_t)(7 - i) * n_dist + d];
+#pragma unroll
+    for (int j = 0; j < kHL; j++) {
+      const int bit = j * kLimbBits, wi = bit >> 5, sh = bit & 31;
+      const uint64_t v = ((uint64_t)(wi + 1 < 8 ? hw[wi + 1] : 0u) << 32) | hw[wi];
+      hl[j] = (uint32_t)(v >> sh) & kLimbMask;
+    }
+  }
+  __syncthreads();  // barrier 2: t written
+  const v4i* wl = w + lane;
+  cptr cn = as_const(fold[key].cnc);
+  asm volatile("" : "+s"(cn));
+  if (two) {  // each contains barrier 3
+    if (wv == 0) lat_fold<0, true, true>(wl, cn, xr, lane, hl);
+    else if (wv == 1) lat_fold<1, true, true>(wl, cn, xr, lane, hl);
+    else if (wv == 2) lat_fold<2, true, true>(wl, cn, xr, lane, hl);
+    else lat_fold<3, true, true>(wl, cn, xr, lane, hl);
+  } else {
+    if (wv == 0) lat_fold<0, false, true>(wl, cn, xr, lane, hl);
+    else if (wv == 1) lat_fold<1, false, true>(wl, cn, xr, lane, hl);
+    else if (wv == 2) lat_fold<2, false, true>(wl, cn, xr, lane, hl);
+    else lat_fold<3, false, true>(wl, cn, xr, lane, hl);
+  }
+  __syncthreads();  // barrier 4: every (p, h) pair written
+  if (wv != 0) return;
+  // D = sum_q (h_q 2^16 + p_q) 2^(28 q), normalised (fold_reduce's carry chain)
+  uint32_t x[kL];
+  {
+    int64_t carry = 0;
+#pragma unroll
+    for (int q = 0; q < kL; q++) {
+      const int64_t v = mad_i64((int)xr[2 * q + 1][lane], 65536, mad_i64((int)xr[2 * q][lane], 1, carry));
+      x[q] = (uint32_t)v & kLimbMask;
+      carry = v >> kLimbBits;
+    }
+  }
+  // s < n, then D' = (D + m n) / 2^28 == n (final_slot)
+  const KeyEntry* ke = keys + key;
+  const cptr n = as_const(ke->n);
+  int32_t br = 0;
+#pragma unroll
+  for (int j = 0; j < kL; j++) br = ((int32_t)sv[j] - (int32_t)n[j] - br) < 0 ? 1 : 0;
+  const uint32_t n0inv = *as_const(&ke->n0inv);
+  const uint32_t m = (x[0] * n0inv) & kLimbMask;
+  uint64_t c = mad64(m, n[0], x[0]) >> kLimbBits;  // the low 28 bits cancel
+  uint32_t diff = 0;
+#pragma unroll
+  for (int k = 1; k < kL; k++) {
+    const uint64_t acc = mad64(m, n[k], x[k] + c);
+    diff |= ((uint32_t)acc & kLimbMask) ^ n[k - 1];
+    c = acc >> kLimbBits;
+  }
+  diff |= c != (uint64_t)n[kL - 1] ? 1u : 0u;
+  if (active) {
+    const bool ok = br != 0 && diff == 0;
+    flags[g] = (uint8_t)(fl | (ok ? MOCHI_GRANT_SIG_OK : 0));
+  }
+}
+
+// MOCHI_NO_FINAL_LAT=1 (A/B): small batches take k_rsa_final as well
+static bool final_lat_off() {
+  static const bool off = [] {
+    const char* e = getenv("MOCHI_NO_FINAL_LAT");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
 }  // namespace
 
-void launch_rsa_final(const LaunchArgs& a, const uint32_t* lead, uint32_t n_dist, hipStream_t st) {
+void launch_rsa_final(const LaunchArgs& a, const uint32_t* lead, uint32_t n_dist, hipStream_t st, bool latency) {
   if (a.dbg_y) {  // mochi_rsa_public_op: materialise s^65537 mod n
     launch_rsa_raw(a, st);
+    return;
+  }
+  if (latency && !final_lat_off()) {  // a small batch: one block per 64-slot chunk (empty chunks exit at once)
+    const uint32_t chunks = (a.n_slots + kLatChunk - 1) / kLatChunk;
+    if (chunks)
+      hipLaunchKernelGGL(k_rsa_final_lat, dim3(chunks), dim3(256), 0, st, a.perm, a.n_slots, a.sig, a.signer, a.keys,
+                         a.fold, a.xbuf, a.digest, lead, n_dist, a.flags);
     return;
   }
   const uint32_t blocks = fold_grid(a.n_slots);

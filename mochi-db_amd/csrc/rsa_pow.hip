@@ -57,9 +57,6 @@
 #ifndef MOCHI_LAT_RAW
 #define MOCHI_LAT_RAW 0
 #endif
-#ifndef MOCHI_LAT_SEQ_TILES
-#define MOCHI_LAT_SEQ_TILES 0  // A/B: k_rsa_pow_lat's M-tiles one after the other
-#endif
 #ifndef MOCHI_LAT_ONE_TILE
 #define MOCHI_LAT_ONE_TILE 1  // A/B (0): k_rsa_pow_lat always folds both N-tiles
 #endif
@@ -162,9 +159,6 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
       continue;
     }
     const uint32_t key = __builtin_amdgcn_readfirstlane((uint32_t)a.signer[g_lead]);
-  // a signature among slots 32-63 (else the fold's second N-tile is skipped)
-  const bool two = MOCHI_LAT_ONE_TILE == 0 ||
-                   __builtin_amdgcn_readfirstlane(base + 32 < a.n_slots && a.perm[base + 32] != 0xFFFFFFFFu);
     if (key != cur_key) {
       __syncthreads();  // the old image is no longer read
       const v4i* src = (const v4i*)a.fold[key].img;
@@ -262,111 +256,6 @@ __global__ __launch_bounds__(512, 1) void k_rsa_pow(const PowArgs a) {
 // through it.  Five block barriers per squaring; one block per CU (the image +
 // 38 KB of exchange), one wave per SIMD.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kLatChunk = 64;
-constexpr int kLatRows = 2 * kL + 1;  // 149 rows: H + M, then t (148), then the (p, h) pairs (148)
-
-// The (p, h) halves of output limb q of an M-tile from its accumulators (the
-// MFMA layout: half h of the wave holds limb 2u + h of both N-tiles'
-// signatures; one swap per half turns them into this lane's own limbs)
-template <int MT>
-__device__ __forceinline__ void lat_assemble(const v16i& d0, const v16i& d1, cptr cadd,
-                                             const uint32_t (*xr)[kLatChunk], uint32_t lane, int (&po)[8], int (&ho)[8]) {
-  int p0[4], h0[4], p1[4], h1[4];
-  static_for<0, 4>([&](auto uc) {
-    constexpr int u = decltype(uc)::value;
-    p0[u] = d0[4 * u] + (d0[4 * u + 1] << 8);
-    h0[u] = d0[4 * u + 2] + (d0[4 * u + 3] << 8);
-    p1[u] = d1[4 * u] + (d1[4 * u + 1] << 8);
-    h1[u] = d1[4 * u + 2] + (d1[4 * u + 3] << 8);
-    swap32(p0[u], p1[u]);  // p0: own limb 2u, p1: own limb 2u + 1
-    swap32(h0[u], h1[u]);
-  });
-  static_for<0, 8>([&](auto rc) {
-    constexpr int r = decltype(rc)::value;
-    constexpr int q = 8 * MT + r, u = r >> 1;
-    if constexpr (q < kL) {
-      int p = (r & 1) ? p1[u] : p0[u];
-      if constexpr (q < kFoldF) p += (int)xr[q][lane];  // t_lo (signed Karatsuba limbs)
-      p += (int)cadd[q];
-      po[r] = p;
-      ho[r] = (r & 1) ? h1[u] : h0[u];
-    }
-  });
-}
-
-// The M-tiles MT0, MT0 + 4, MT0 + 8 (< 10) of one wave, their K-steps
-// interleaved (4-6 independent MFMA chains: alone on its SIMD a wave would
-// otherwise wait out each chain's latency), then -- once the block has finished
-// reading t (barrier 3, inside) -- the (p, h) pairs stored at rows 2q, 2q + 1.
-// !kTwo: slots 32-63 of the chunk are empty (a bucket fills from its start), so
-// the second N-tile (signatures 32-63) is skipped -- half the MFMAs; lanes
-// 32-63 then carry garbage, and they are never stored (a batcher flush of a few
-// messages has 1-2 grants per signer bucket).
-template <int MT0, bool kTwo>
-__device__ __forceinline__ void lat_fold(const v4i* wl, cptr cadd, uint32_t (*xr)[kLatChunk], uint32_t lane) {
-  constexpr int NT = MT0 + 8 < kFoldMT ? 3 : 2;
-  v4i b0[kFoldKS], b1[kFoldKS];
-  static_for<0, kFoldKS>([&](auto sc) {
-    constexpr int s = decltype(sc)::value;
-    static_for<0, 4>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      constexpr int jp = 8 * s + i, jq = 8 * s + 4 + i;
-      int p = 0, q = 0;  // t_hi arrives biased (kara_combine); padding K slots have zero weights
-      if constexpr (jp < kFoldNH) p = (int)xr[kFoldF + jp][lane];
-      if constexpr (jq < kFoldNH) q = (int)xr[kFoldF + jq][lane];
-      swap32(p, q);
-      b0[s][i] = p;
-      b1[s][i] = q;
-    });
-  });
-  v16i d0[NT], d1[NT];
-  static_for<0, NT>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    d0[j] = v16i{};
-    d1[j] = v16i{};
-  });
-#if MOCHI_LAT_SEQ_TILES
-  static_for<0, NT>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    static_for<0, kFoldKS>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
-      d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
-      if constexpr (kTwo) d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  });
-#else
-  static_for<0, kFoldKS>([&](auto sc) {
-    constexpr int s = decltype(sc)::value;
-    static_for<0, NT>([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      const v4i a = wl[((MT0 + 4 * j) * kFoldKS + s) * 64];
-      d0[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0[s], d0[j], 0, 0, 0);
-      if constexpr (kTwo) d1[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1[s], d1[j], 0, 0, 0);
-    });
-  });
-#endif
-  int po[3][8] = {}, ho[3][8] = {};
-  static_for<0, NT>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    lat_assemble<MT0 + 4 * j>(d0[j], d1[j], cadd, xr, lane, po[j], ho[j]);
-  });
-  __syncthreads();  // barrier 3: every wave is done reading t
-  static_for<0, NT>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    constexpr int mt = MT0 + 4 * j;
-    static_for<0, 8>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      constexpr int q = 8 * mt + r;
-      if constexpr (q < kL) {
-        xr[2 * q][lane] = (uint32_t)po[j][r];
-        xr[2 * q + 1][lane] = (uint32_t)ho[j][r];
-      }
-    });
-  });
-}
-
 // A 37-limb square's columns as independent 64-bit sums (no carry between
 // them, so the scheduler interleaves the chains -- a wave alone on its SIMD
 // would wait out each mad's latency along one chain), then one carry pass into
@@ -434,6 +323,7 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
   __syncthreads();
   const cptr c = as_const(a.fold[key].cadd);
   const v4i* wl = w + lane;
+  const uint32_t kNoH[kHL] = {};  // nothing subtracted (k_rsa_final_lat subtracts the digest)
 #pragma unroll 1
   for (int it = 0; it < 16; it++) {
     uint32_t lv[kL];
@@ -492,15 +382,15 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
     cptr ci = c;
     asm volatile("" : "+s"(ci));
     if (two) {  // each contains barrier 3
-      if (wv == 0) lat_fold<0, true>(wl, ci, xr, lane);
-      else if (wv == 1) lat_fold<1, true>(wl, ci, xr, lane);
-      else if (wv == 2) lat_fold<2, true>(wl, ci, xr, lane);
-      else lat_fold<3, true>(wl, ci, xr, lane);
+      if (wv == 0) lat_fold<0, true>(wl, ci, xr, lane, kNoH);
+      else if (wv == 1) lat_fold<1, true>(wl, ci, xr, lane, kNoH);
+      else if (wv == 2) lat_fold<2, true>(wl, ci, xr, lane, kNoH);
+      else lat_fold<3, true>(wl, ci, xr, lane, kNoH);
     } else {
-      if (wv == 0) lat_fold<0, false>(wl, ci, xr, lane);
-      else if (wv == 1) lat_fold<1, false>(wl, ci, xr, lane);
-      else if (wv == 2) lat_fold<2, false>(wl, ci, xr, lane);
-      else lat_fold<3, false>(wl, ci, xr, lane);
+      if (wv == 0) lat_fold<0, false>(wl, ci, xr, lane, kNoH);
+      else if (wv == 1) lat_fold<1, false>(wl, ci, xr, lane, kNoH);
+      else if (wv == 2) lat_fold<2, false>(wl, ci, xr, lane, kNoH);
+      else lat_fold<3, false>(wl, ci, xr, lane, kNoH);
     }
     __syncthreads();  // barrier 4: every (p, h) pair written
     if (wv < 3) {  // x' = sum_q (h_q 2^16 + p_q) 2^(28 q), normalised (fold_reduce's carry chain)
