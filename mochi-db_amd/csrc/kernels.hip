@@ -481,25 +481,39 @@ __global__ __launch_bounds__(1024) void k_bucket_small(const uint16_t* __restric
     if (k < n_keys) atomicAdd(&cnt[k], 1u);
   }
   __syncthreads();
-  // exclusive scan of the 512-aligned bucket sizes: per-thread runs, then thread 0 over the 1024 partials
+  // exclusive scan of the 512-aligned bucket sizes: per-thread runs, a shuffle
+  // scan per wave, then one over the 16 wave totals (a serial pass of thread 0
+  // over the 1024 partials was most of this kernel's time)
   const uint32_t per = (n_keys + blockDim.x - 1) / blockDim.x, b = threadIdx.x * per;
   uint32_t sum = 0;
   for (uint32_t k = b; k < b + per && k < n_keys; k++) sum += (cnt[k] + kBucketAlign - 1) & ~(kBucketAlign - 1);
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (uint32_t t = 0; t < blockDim.x; t++) {
-      const uint32_t v = part[t];
-      part[t] = run;
-      run += v;
-    }
-    total[0] = run;
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t incl = sum;
 #pragma unroll
-    for (int i = 1; i < kTotalWords; i++) total[i] = 0;  // the counters of this call's later kernels (kernels.h)
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) part[wid] = incl;
+  __syncthreads();
+  if (wid == 0) {
+    const uint32_t nw = blockDim.x >> 6;  // 16 wave totals
+    const uint32_t wt = lane < nw ? part[lane] : 0u;
+    uint32_t wi = wt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(wi, d, 64);
+      if (lane >= (uint32_t)d) wi += y;
+    }
+    if (lane < nw) part[64 + lane] = wi - wt;  // exclusive
+    if (lane == nw - 1) {
+      total[0] = wi;
+#pragma unroll
+      for (int i = 1; i < kTotalWords; i++) total[i] = 0;  // the counters of this call's later kernels (kernels.h)
+    }
   }
   __syncthreads();
-  uint32_t run = part[threadIdx.x];
+  uint32_t run = part[64 + wid] + incl - sum;
   for (uint32_t k = b; k < b + per && k < n_keys; k++) {
     cur[k] = run;
     run += (cnt[k] + kBucketAlign - 1) & ~(kBucketAlign - 1);
