@@ -1231,6 +1231,41 @@ __device__ __forceinline__ void emit_grant(const W2Out& out, uint32_t g, uint64_
   out.grant_key[g] = key;
 }
 
+// A small batch (M < kW2SmallM messages) runs the decode's two scans inside
+// one 1024-thread block of the kernel after each (k_w2_entries, k_w2_final)
+// instead of as hipcub launches of their own: each launch is ~5 us of dispatch
+// on an otherwise idle GPU, a batcher flush carries one or two messages.
+constexpr uint32_t kW2SmallM = 1024;
+
+// Exclusive scan of v over the 1024 threads of the block (16 waves): a shuffle
+// scan per wave, then one over the wave totals.  lds: 33 words of its own (a
+// second scan in the same kernel takes other words); total = the block's sum.
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t* lds, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) lds[wid] = incl;
+  __syncthreads();
+  if (wid == 0) {
+    const uint32_t wt = lane < nw ? lds[lane] : 0u;
+    uint32_t wi = wt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(wi, d, 64);
+      if (lane >= (uint32_t)d) wi += y;
+    }
+    if (lane < nw) lds[16 + lane] = wi - wt;
+    if (lane == nw - 1) lds[32] = wi;
+  }
+  __syncthreads();
+  total = lds[32];
+  return lds[16 + wid] + incl - v;
+}
+
 // Level 1.  cnt_o[m] = operations on the wire (k_w2_final turns it into the
 // decoded count).  Element M of cnt_ce is the scan's extra element.
 // three waves per SIMD (the register cap keeps the level-1 walk at the occupancy
@@ -1263,13 +1298,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOCHI_W2MSG
 }
 
 // Level 1, second walk: the certificate entries into the compact list.
-__global__ __launch_bounds__(256) void k_w2_entries(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
-                                                    const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce) {
+// kSmall: one block, M < kW2SmallM; the entry offsets (ce_base, the scan of
+// cnt_ce) are computed here first.
+template <bool kSmall>
+__global__ __launch_bounds__(kSmall ? 1024 : 256) void k_w2_entries(const uint8_t* __restrict__ wire,
+                                                                    const uint64_t* __restrict__ moff,
+                                                                    const uint32_t* __restrict__ mlen, uint32_t M,
+                                                                    W2Msg s, CE ce) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t e;
+  if constexpr (kSmall) {
+    __shared__ uint32_t lds[33];
+    const uint32_t v = m < M ? s.cnt_ce[m] : 0u;
+    uint32_t total;
+    e = block_scan_excl(v, lds, total);
+    if (m <= M) s.ce_base[m] = e;  // ce_base[M] = the entry total (k_w2_mg, k_w2_emit_mg)
+  }
   if (m >= M) return;
   const uint32_t nce = s.cnt_ce[m];
   if (nce == 0) return;
-  uint32_t e = s.ce_base[m];
+  if constexpr (!kSmall) e = s.ce_base[m];
   if (nce <= kW2InlEntries) {  // recorded by level 1: copy
     const uint4* q = (const uint4*)(s.inl + (size_t)4 * kW2InlEntries * m);
 #pragma unroll 4
@@ -1464,23 +1512,17 @@ __global__ __launch_bounds__(256) MOCHI_W2MG_ATTR void k_w2_mg(
   stp.store();
 }
 
-// Per message: final status and the decoded counts.
-__global__ __launch_bounds__(256) void k_w2_final(uint32_t M, const uint32_t* __restrict__ flags_off, W2Msg s, CE ce,
-                                                  uint32_t* __restrict__ cnt_g, uint32_t* __restrict__ cnt_m,
-                                                  uint8_t* __restrict__ status, uint4* __restrict__ cnt4) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m > M) return;
-  if (m == M) {  // the scan's extra element: totals land at [M]
-    cnt_g[M] = 0;
-    s.cnt_o[M] = 0;
-    cnt_m[M] = 0;
-    cnt4[M] = make_uint4(0, 0, 0, 0);
-    return;
-  }
+// Per message: final status and the decoded counts (k_w2_final).
+__device__ __forceinline__ void w2_final_msg(uint32_t m, const uint32_t* __restrict__ flags_off, const W2Msg& s,
+                                             const CE& ce, uint32_t* __restrict__ cnt_g, uint32_t* __restrict__ cnt_m,
+                                             uint8_t* __restrict__ status, uint4* __restrict__ cnt4, uint32_t& ng,
+                                             uint32_t& no, uint32_t& nm) {
   uint32_t bits = s.st_bits[m];
   if ((bits & kStAssume) && (bits & kStFirstNC)) bits |= kStFb;  // a lane's assumed-canonical grant was not
   uint32_t st = (bits & kStMal) ? MOCHI_MSG_MALFORMED : (bits & kStFb) ? MOCHI_MSG_FALLBACK : MOCHI_MSG_OK;
-  uint32_t no = s.cnt_o[m], ng = 0, nm = 0;
+  no = s.cnt_o[m];
+  ng = 0;
+  nm = 0;
   if (st == MOCHI_MSG_OK && flags_off && flags_off[m + 1] - flags_off[m] != no) st = MOCHI_MSG_OPS_MISMATCH;
   if (st == MOCHI_MSG_OK) {
 #pragma unroll 1
@@ -1499,6 +1541,44 @@ __global__ __launch_bounds__(256) void k_w2_final(uint32_t M, const uint32_t* __
   cnt_m[m] = nm;
   cnt4[m] = make_uint4(ng, no, nm, 0);
   status[m] = (uint8_t)st;
+}
+
+// kSmall: one block, M < kW2SmallM; the packed scan of (grants, ops,
+// MultiGrants) into off4 is done here as well.
+template <bool kSmall>
+__global__ __launch_bounds__(kSmall ? 1024 : 256) void k_w2_final(uint32_t M, const uint32_t* __restrict__ flags_off,
+                                                                  W2Msg s, CE ce, uint32_t* __restrict__ cnt_g,
+                                                                  uint32_t* __restrict__ cnt_m,
+                                                                  uint8_t* __restrict__ status, uint4* __restrict__ cnt4,
+                                                                  uint4* __restrict__ off4) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (kSmall) {
+    __shared__ uint32_t lds[3][33];
+    uint32_t ng = 0, no = 0, nm = 0;
+    if (m < M) w2_final_msg(m, flags_off, s, ce, cnt_g, cnt_m, status, cnt4, ng, no, nm);
+    uint32_t tg, to, tm;
+    const uint32_t eg = block_scan_excl(ng, lds[0], tg), eo = block_scan_excl(no, lds[1], to),
+                   em = block_scan_excl(nm, lds[2], tm);
+    if (m < M) off4[m] = make_uint4(eg, eo, em, 0);
+    if (m == M) {
+      cnt_g[M] = 0;
+      s.cnt_o[M] = 0;
+      cnt_m[M] = 0;
+      cnt4[M] = make_uint4(0, 0, 0, 0);
+      off4[M] = make_uint4(tg, to, tm, 0);  // the totals (the host reads them)
+    }
+    return;
+  }
+  if (m > M) return;
+  if (m == M) {  // the scan's extra element: totals land at [M]
+    cnt_g[M] = 0;
+    s.cnt_o[M] = 0;
+    cnt_m[M] = 0;
+    cnt4[M] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  uint32_t ng, no, nm;
+  w2_final_msg(m, flags_off, s, ce, cnt_g, cnt_m, status, cnt4, ng, no, nm);
 }
 
 // Emit, lane = certificate entry: a key's first entry writes its MultiGrant
@@ -1699,6 +1779,15 @@ hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes) {
   return e;
 }
 
+// MOCHI_W2_NO_SMALL_SCAN=1 (A/B): small batches scan with hipcub too
+static bool small_scan_off() {
+  static const bool off = [] {
+    const char* e = getenv("MOCHI_W2_NO_SMALL_SCAN");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
 hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
   const W2Msg s = msg_view(a);
   const CE ce = ce_view(a.ce, a.ce_cap);
@@ -1706,16 +1795,26 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
   hipLaunchKernelGGL(k_w2_msg, dim3(gm1), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (a.M < kW2SmallM && !small_scan_off()) {  // the scans inside single-block kernels
+    hipLaunchKernelGGL(k_w2_entries<true>, dim3(1), dim3(1024), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce);
+    if (a.M)
+      hipLaunchKernelGGL(k_w2_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce, a.ids,
+                         a.id_off, a.n_ids);
+    hipLaunchKernelGGL(k_w2_final<true>, dim3(1), dim3(1024), 0, st, a.M, a.flags_off, s, ce, a.cnt_g, a.cnt_m,
+                       a.status, (uint4*)a.cnt4, (uint4*)a.off4);
+    return hipGetLastError();
+  }
   size_t tb = a.scan_temp_bytes;
   e = hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, s.cnt_ce, s.ce_base, (int)(a.M + 1), st);
   if (e != hipSuccess) return e;
   if (a.M) {
-    hipLaunchKernelGGL(k_w2_entries, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce);
+    hipLaunchKernelGGL(k_w2_entries<false>, dim3(cdiv(a.M, 256)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M,
+                       s, ce);
     hipLaunchKernelGGL(k_w2_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce, a.ids,
                        a.id_off, a.n_ids);
   }
-  hipLaunchKernelGGL(k_w2_final, dim3(gm1), dim3(256), 0, st, a.M, a.flags_off, s, ce, a.cnt_g, a.cnt_m, a.status,
-                     (uint4*)a.cnt4);
+  hipLaunchKernelGGL(k_w2_final<false>, dim3(gm1), dim3(256), 0, st, a.M, a.flags_off, s, ce, a.cnt_g, a.cnt_m,
+                     a.status, (uint4*)a.cnt4, (uint4*)a.off4);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   // one scan of the packed (grants, ops, MultiGrants) counts instead of three
