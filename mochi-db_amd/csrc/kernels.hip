@@ -466,9 +466,15 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint16_t* __restri
 // memsets and three kernels, each ~5 us of dispatch on an otherwise idle GPU.
 constexpr uint32_t kSmallGrants = 4096;
 
+// prep (n <= kSmallPrepFused): then the per-grant prep of the n grants as
+// well, in the same block (one launch fewer; nothing reads the prep's outputs
+// before k_rsa_final).
+constexpr uint32_t kSmallPrepFused = 1024;
+
 __global__ __launch_bounds__(1024) void k_bucket_small(const uint16_t* __restrict__ signer, uint32_t n, uint32_t n_keys,
                                                        uint32_t n_slots, uint32_t* __restrict__ perm,
-                                                       uint32_t* __restrict__ total) {
+                                                       uint32_t* __restrict__ total, const PrepArgs pa,
+                                                       uint32_t prep) {
   extern __shared__ uint32_t lds[];  // [n_keys] count, then [n_keys] cursor
   uint32_t* cnt = lds;
   uint32_t* cur = lds + n_keys;
@@ -523,6 +529,8 @@ __global__ __launch_bounds__(1024) void k_bucket_small(const uint16_t* __restric
     const uint32_t k = signer[i];
     if (k < n_keys) perm[atomicAdd(&cur[k], 1u)] = i;
   }
+  if (prep)
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) grant_prep_one(pa, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -902,6 +910,15 @@ static bool hash_precheck() {
   return on;
 }
 
+// MOCHI_W2_NO_SMALL_SCAN=1 (A/B, with the decoder's): the small-batch prep as a launch of its own
+static bool small_scan_off() {
+  static const bool off = [] {
+    const char* e = getenv("MOCHI_W2_NO_SMALL_SCAN");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
 // MOCHI_NO_SMALL=1 (A/B): small batches take the large-batch launch sequence
 static bool small_off() {
   static const bool off = [] {
@@ -957,12 +974,14 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
   const uint32_t* lead = dedup ? a.lead : nullptr;
   const bool prep = N && !a.skip_prep_tally;
   const bool fork = prep && a.aux && !small;
+  // a small batch of at most kSmallPrepFused grants: the prep inside k_bucket_small
+  const bool prep_fused = small && prep && N <= kSmallPrepFused && !small_scan_off();
   hipStream_t ps = fork ? a.aux : st;
   auto bucket = [&](hipStream_t bs) -> hipError_t {
     mark(kStageBucket, false, bs);
     if (small) {
       hipLaunchKernelGGL(k_bucket_small, dim3(1), dim3(1024), 2 * sizeof(uint32_t) * a.n_keys, bs, a.signer, N,
-                         a.n_keys, a.n_slots, a.perm, a.total);
+                         a.n_keys, a.n_slots, a.perm, a.total, pa, (uint32_t)prep_fused);
     } else if (N) {
       hipError_t e = hipMemsetAsync(a.count, 0, sizeof(uint32_t) * a.n_keys, bs);
       if (e != hipSuccess) return e;
@@ -990,7 +1009,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
         const uint32_t mblocks = cdiv(N, 4 * 256) < 2048 ? cdiv(N, 4 * 256) : 2048;  // 4 waves x 256 grants
         hipLaunchKernelGGL(k_grant_match, dim3(mblocks), dim3(256), 0, ps, pa, a.rare);
         hipLaunchKernelGGL(k_grant_prep_rare, dim3(cdiv(N, kRareSpan)), dim3(256), 0, ps, pa, (const uint8_t*)a.rare);
-      } else {
+      } else if (!prep_fused) {
         hipLaunchKernelGGL(k_grant_prep, dim3(cdiv(N, 256)), dim3(256), 0, ps, pa);
       }
     }

@@ -1583,6 +1583,47 @@ __global__ __launch_bounds__(kSmall ? 1024 : 256) void k_w2_final(uint32_t M, co
 
 // Emit, lane = certificate entry: a key's first entry writes its MultiGrant
 // (the final value's grants) at the position its predecessors leave.
+// Certificate entry e: a key's first entry writes its MultiGrant.
+__device__ __forceinline__ void emit_mg_entry(uint32_t e, const uint8_t* __restrict__ wire,
+                                              const uint64_t* __restrict__ moff, const uint32_t* __restrict__ mlen,
+                                              const W2Msg& s, const CE& ce, const uint8_t* __restrict__ status,
+                                              const uint4* __restrict__ off4, const uint8_t* __restrict__ ids,
+                                              const uint32_t* __restrict__ id_off, uint32_t n_ids, const W2Out& out) {
+  const uint32_t L = ce.last[e];
+  if (L == ~0u) return;
+  const uint32_t m = ce.msg[e];
+  if (status[m] != MOCHI_MSG_OK) return;
+  uint32_t idx = 0, gb = 0;
+#pragma unroll 1
+  for (uint32_t j = s.ce_base[m]; j < e; j++) {
+    const uint32_t Lj = ce.last[j];
+    if (Lj != ~0u) {
+      idx++;
+      gb += ce.ng[Lj];
+    }
+  }
+  const uint4 base = off4[m];  // (grants, ops, MultiGrants) before message m
+  uint32_t g = base.x + gb;
+  out.mg_grant_off[base.z + idx] = g;  // this MultiGrant's first grant
+  const uint64_t mo = moff[m];
+  if (ce.ng[L] == 1) {  // recorded by k_w2_mg
+    const uint32_t sk = ce.r_sk[L];
+    // the same bytes as the message's first grant -- the first one emitted
+    // (base.x) when the first entry holds its key's final value, one grant
+    const uint32_t b0 = s.ce_base[m];
+    const bool same = (sk >> 31) && L != b0 && ce.last[b0] == b0 && ce.ng[b0] == 1 && ((ce.r_sk[b0] >> 30) & 1u);
+    emit_grant(out, g, mo, ce.r_goff[L], ce.r_glen[L], (uint16_t)(sk >> 8), ce.r_sig[L], (uint8_t)sk,
+               same ? base.x : ~0u);
+    return;
+  }
+  ByteReader r;
+  r.init(wire + mo, mlen[m]);
+  walk_mg(r, ce.voff[L], ce.vlen[L], s.tx_off[m], s.tx_len[m], ids, id_off, n_ids,
+          [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
+            emit_grant(out, g++, mo, go, gl, sg, so, key);
+          });
+}
+
 __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
                                                     const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce,
                                                     const uint8_t* __restrict__ status,
@@ -1590,54 +1631,20 @@ __global__ __launch_bounds__(256) void k_w2_emit_mg(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ id_off, uint32_t n_ids, W2Out out) {
   const uint32_t total = s.ce_base[M];
 #pragma unroll 1
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-    const uint32_t L = ce.last[e];
-    if (L == ~0u) continue;
-    const uint32_t m = ce.msg[e];
-    if (status[m] != MOCHI_MSG_OK) continue;
-    uint32_t idx = 0, gb = 0;
-#pragma unroll 1
-    for (uint32_t j = s.ce_base[m]; j < e; j++) {
-      const uint32_t Lj = ce.last[j];
-      if (Lj != ~0u) {
-        idx++;
-        gb += ce.ng[Lj];
-      }
-    }
-    const uint4 base = off4[m];  // (grants, ops, MultiGrants) before message m
-    uint32_t g = base.x + gb;
-    out.mg_grant_off[base.z + idx] = g;  // this MultiGrant's first grant
-    const uint64_t mo = moff[m];
-    if (ce.ng[L] == 1) {  // recorded by k_w2_mg
-      const uint32_t sk = ce.r_sk[L];
-      // the same bytes as the message's first grant -- the first one emitted
-      // (base.x) when the first entry holds its key's final value, one grant
-      const uint32_t b0 = s.ce_base[m];
-      const bool same = (sk >> 31) && L != b0 && ce.last[b0] == b0 && ce.ng[b0] == 1 && ((ce.r_sk[b0] >> 30) & 1u);
-      emit_grant(out, g, mo, ce.r_goff[L], ce.r_glen[L], (uint16_t)(sk >> 8), ce.r_sig[L], (uint8_t)sk,
-                 same ? base.x : ~0u);
-      continue;
-    }
-    ByteReader r;
-    r.init(wire + mo, mlen[m]);
-    walk_mg(r, ce.voff[L], ce.vlen[L], s.tx_off[m], s.tx_len[m], ids, id_off, n_ids,
-            [&](uint32_t go, uint32_t gl, uint16_t sg, uint32_t so, uint8_t key) {
-              emit_grant(out, g++, mo, go, gl, sg, so, key);
-            });
-  }
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x)
+    emit_mg_entry(e, wire, moff, mlen, s, ce, status, off4, ids, id_off, n_ids, out);
 }
 
 // Emit, lane = message: the operations (key slot = index of the first op
 // naming the same operand1) and the MultiGrant CSR terminator.
-__global__ __launch_bounds__(256) void k_w2_ops(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
-                                                const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s,
-                                                const uint8_t* __restrict__ status, const uint4* __restrict__ off4,
-                                                uint32_t* __restrict__ g_base, uint32_t* __restrict__ o_base,
-                                                uint32_t* __restrict__ m_base, const uint32_t* __restrict__ flags_off,
-                                                const uint8_t* __restrict__ flags_in,
-                                                const int64_t* __restrict__ ots_in, W2Out out) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m > M) return;
+__device__ __forceinline__ void emit_ops_msg(uint32_t m, const uint8_t* __restrict__ wire,
+                                             const uint64_t* __restrict__ moff, const uint32_t* __restrict__ mlen,
+                                             uint32_t M, const W2Msg& s, const uint8_t* __restrict__ status,
+                                             const uint4* __restrict__ off4, uint32_t* __restrict__ g_base,
+                                             uint32_t* __restrict__ o_base, uint32_t* __restrict__ m_base,
+                                             const uint32_t* __restrict__ flags_off,
+                                             const uint8_t* __restrict__ flags_in, const int64_t* __restrict__ ots_in,
+                                             const W2Out& out) {
   // the packed scan unpacked into the batch's three CSR arrays ([M] = totals)
   const uint4 base = off4[m];
   g_base[m] = base.x;
@@ -1688,13 +1695,22 @@ __global__ __launch_bounds__(256) void k_w2_ops(const uint8_t* __restrict__ wire
   }
 }
 
+__global__ __launch_bounds__(256) void k_w2_ops(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ moff,
+                                                const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s,
+                                                const uint8_t* __restrict__ status, const uint4* __restrict__ off4,
+                                                uint32_t* __restrict__ g_base, uint32_t* __restrict__ o_base,
+                                                uint32_t* __restrict__ m_base, const uint32_t* __restrict__ flags_off,
+                                                const uint8_t* __restrict__ flags_in,
+                                                const int64_t* __restrict__ ots_in, W2Out out) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m <= M) emit_ops_msg(m, wire, moff, mlen, M, s, status, off4, g_base, o_base, m_base, flags_off, flags_in, ots_in, out);
+}
+
 // sig[g] = wire[sig_src[g] .. +256) (zeros when absent): 16 lanes per grant,
 // each moving 16 bytes, so a wave reads 4 signatures' contiguous bytes.
-__global__ __launch_bounds__(256) void k_w2_sig(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ sig_src,
-                                                uint32_t N, uint8_t* __restrict__ sig) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void emit_sig_piece(uint64_t t, const uint8_t* __restrict__ wire,
+                                               const uint64_t* __restrict__ sig_src, uint8_t* __restrict__ sig) {
   const uint32_t g = (uint32_t)(t >> 4), q = (uint32_t)(t & 15);
-  if (g >= N) return;
   const uint64_t src = sig_src[g];
   uint4 v = make_uint4(0, 0, 0, 0);
   if (src != ~0ull) {
@@ -1719,6 +1735,40 @@ __global__ __launch_bounds__(256) void k_w2_sig(const uint8_t* __restrict__ wire
                    __builtin_amdgcn_alignbit(e[3], e[2], r), __builtin_amdgcn_alignbit(e[4], e[3], r));
   }
   ((uint4*)(sig + (size_t)g * MOCHI_RSA_BYTES))[q] = v;
+}
+
+__global__ __launch_bounds__(256) void k_w2_sig(const uint8_t* __restrict__ wire, const uint64_t* __restrict__ sig_src,
+                                                uint32_t N, uint8_t* __restrict__ sig) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((t >> 4) < N) emit_sig_piece(t, wire, sig_src, sig);
+}
+
+// A small batch (M < kW2SmallM): the three emit kernels above as one block
+// (entries, then messages, then -- once every grant's signature source is
+// written -- the signatures), two launches fewer after the host has read the
+// decoded totals.
+__global__ __launch_bounds__(1024) void k_w2_emit_small(const uint8_t* __restrict__ wire,
+                                                         const uint64_t* __restrict__ moff,
+                                                         const uint32_t* __restrict__ mlen, uint32_t M, W2Msg s, CE ce,
+                                                         const uint8_t* __restrict__ status,
+                                                         const uint4* __restrict__ off4,
+                                                         const uint8_t* __restrict__ ids,
+                                                         const uint32_t* __restrict__ id_off, uint32_t n_ids,
+                                                         uint32_t* __restrict__ g_base, uint32_t* __restrict__ o_base,
+                                                         uint32_t* __restrict__ m_base,
+                                                         const uint32_t* __restrict__ flags_off,
+                                                         const uint8_t* __restrict__ flags_in,
+                                                         const int64_t* __restrict__ ots_in, uint32_t N, W2Out out) {
+  const uint32_t total = s.ce_base[M];
+#pragma unroll 1
+  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x)
+    emit_mg_entry(e, wire, moff, mlen, s, ce, status, off4, ids, id_off, n_ids, out);
+#pragma unroll 1
+  for (uint32_t m = threadIdx.x; m <= M; m += blockDim.x)
+    emit_ops_msg(m, wire, moff, mlen, M, s, status, off4, g_base, o_base, m_base, flags_off, flags_in, ots_in, out);
+  __syncthreads();  // sig_src written (emit_grant)
+#pragma unroll 1
+  for (uint64_t t = threadIdx.x; t < (uint64_t)N * 16; t += blockDim.x) emit_sig_piece(t, wire, out.sig_src, out.sig);
 }
 
 __global__ __launch_bounds__(256) void k_w2_fixup(const uint8_t* __restrict__ status, uint32_t M,
@@ -1779,7 +1829,8 @@ hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes) {
   return e;
 }
 
-// MOCHI_W2_NO_SMALL_SCAN=1 (A/B): small batches scan with hipcub too
+// MOCHI_W2_NO_SMALL_SCAN=1 (A/B): small batches take the large-batch decode
+// launches too (hipcub scans, three emit kernels)
 static bool small_scan_off() {
   static const bool off = [] {
     const char* e = getenv("MOCHI_W2_NO_SMALL_SCAN");
@@ -1828,6 +1879,12 @@ hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
           a.op_object_ts, a.op_key_off, a.op_key_len, a.mg_grant_off, a.grant_same};
   const W2Msg s = msg_view(a);
   const CE ce = ce_view(a.ce, a.ce_cap);
+  if (a.M < kW2SmallM && !small_scan_off()) {
+    hipLaunchKernelGGL(k_w2_emit_small, dim3(1), dim3(1024), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce, a.status,
+                       (const uint4*)a.off4, a.ids, a.id_off, a.n_ids, a.cert_grant_off, a.cert_op_off, a.cert_mg_off,
+                       a.flags_off, a.flags_in, a.ots_in, a.N, o);
+    return hipGetLastError();
+  }
   if (a.M)
     hipLaunchKernelGGL(k_w2_emit_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce,
                        a.status, (const uint4*)a.off4, a.ids, a.id_off, a.n_ids, o);
