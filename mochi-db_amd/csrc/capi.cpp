@@ -47,6 +47,14 @@ bool prep_serial() {
   return v;
 }
 
+bool fixup_kernel() {
+  static const bool v = [] {
+    const char* e = getenv("MOCHI_W2_FIXUP_KERNEL");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 uint32_t default_chunk_grants() {
   const char* e = getenv("MOCHI_CHUNK_GRANTS");
   const long x = e ? atol(e) : 0;
@@ -545,7 +553,8 @@ hipError_t scratch_release(mochi_ctx* c, hipStream_t st) {
 int ensure_scratch(mochi_ctx* c, uint32_t N, uint32_t C);
 
 int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_verdicts* o, hipStream_t st,
-               const uint32_t* op_out_off = nullptr, const uint32_t* grant_same = nullptr) {
+               const uint32_t* op_out_off = nullptr, const uint32_t* grant_same = nullptr,
+               const uint8_t* msg_status = nullptr) {
   const uint32_t N = b->n_grants, C = b->n_certs;
   const uint64_t slots = mochi::slot_capacity(N, c->n_keys);
   if (slots > 0xFFFFFFF0ull) return fail(MOCHI_EINVAL, "batch too large");
@@ -603,6 +612,7 @@ int run_device(mochi_ctx* c, const mochi_batch* b, const mochi_params* p, mochi_
   a.op_g0 = o->op_g0;
   a.op_ts = o->op_ts;
   a.op_out_off = op_out_off;
+  a.msg_status = msg_status;
   a.aux = prep_serial() ? nullptr : c->aux;  // MOCHI_PREP_SERIAL=1: prep on the launch stream (A/B)
   a.ev_fork = c->ev_fork;
   a.ev_join = c->ev_join;
@@ -1038,9 +1048,13 @@ int w2_verify(mochi_ctx* c, const mochi_write2_batch* w, const mochi_params* p, 
   dv.op_decision = o->op_decision;
   dv.op_g0 = o->op_g0;
   dv.op_ts = o->op_ts;
-  if ((rc = run_device(c, &db, p, &dv, st, op_out_off, a.grant_same))) return rc;
-  HIP_TRY(mochi::launch_w2_fixup(a, o->cert_accept_bits, o->cert_reason, o->cert_fail_op, o->op_decision, o->op_g0,
-                                 o->op_ts, st));
+  // the status fix-up of undecoded messages runs inside k_tally (one launch
+  // fewer at the end of the call); MOCHI_W2_FIXUP_KERNEL=1 (A/B): as its own kernel
+  const bool fused = !fixup_kernel();
+  if ((rc = run_device(c, &db, p, &dv, st, op_out_off, a.grant_same, fused ? a.status : nullptr))) return rc;
+  if (!fused)
+    HIP_TRY(mochi::launch_w2_fixup(a, o->cert_accept_bits, o->cert_reason, o->cert_fail_op, o->op_decision, o->op_g0,
+                                   o->op_ts, st));
   return MOCHI_OK;
 }
 

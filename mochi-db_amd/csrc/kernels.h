@@ -56,6 +56,9 @@ struct LaunchArgs {
   uint32_t* op_g0;        // [O] may be null
   int64_t* op_ts;         // [O] may be null
   const uint32_t* op_out_off;  // [C+1] per-op output positions; null = cert_op_off
+  // wire path: [C] message status (w2_decode.hip); k_tally applies k_w2_fixup's
+  // overrides to the undecoded messages (else null)
+  const uint8_t* msg_status;
   // mochi_rsa_public_op only: raw s^65537 mod n words [N][64] (else null)
   uint32_t* dbg_y;
   bool skip_prep_tally;

@@ -605,6 +605,7 @@ struct TallyArgs {
   uint32_t* op_g0;
   int64_t* op_ts;
   const uint32_t* op_out_off;
+  const uint8_t* msg_status;  // [n_certs] or null: the wire path's message status
 };
 
 // MOCHI_Q_BIND: Grant.objectId == the op key it is filed under (op `o`'s
@@ -833,6 +834,20 @@ __global__ __launch_bounds__(256) MOCHI_TALLY_ATTR void k_tally(const TallyArgs 
           break;
         }
       }
+    }
+    // the wire path's undecoded messages (k_w2_fixup's overrides, done here in
+    // the same pass): MALFORMED rejected as such, FALLBACK / OPS_MISMATCH left
+    // UNDECIDED for the host's fallback, their wire ops not reached
+    const uint32_t ms = a.msg_status ? a.msg_status[c] : (uint32_t)MOCHI_MSG_OK;
+    if (ms != MOCHI_MSG_OK) {
+      reason = ms == MOCHI_MSG_MALFORMED ? MOCHI_REJECT_MALFORMED : MOCHI_UNDECIDED;
+      fail_op = 0xFF;
+      if (a.op_out_off)
+        for (uint32_t o = a.op_out_off[c]; o < a.op_out_off[c + 1]; o++) {
+          if (a.op_decision) a.op_decision[o] = MOCHI_OPD_SKIPPED;
+          if (a.op_g0) a.op_g0[o] = 0xFFFFFFFFu;
+          if (a.op_ts) a.op_ts[o] = 0;
+        }
     }
     if (a.reason_out) a.reason_out[c] = (uint8_t)reason;
     if (a.fail_op_out) a.fail_op_out[c] = (uint8_t)fail_op;
@@ -1093,6 +1108,7 @@ hipError_t launch_verify(const LaunchArgs& a, hipStream_t st) {
     t.op_g0 = a.op_g0;
     t.op_ts = a.op_ts;
     t.op_out_off = a.op_out_off;
+    t.msg_status = a.msg_status;
     // lean: every slot leader's hash checked in k_grant_prep_cert, no bind mode
     if (dedup && hash_precheck() && !(a.quorum_mode & MOCHI_Q_BIND))
       hipLaunchKernelGGL(k_tally<true>, dim3(cdiv(C, 256)), dim3(256), 0, st, t);
