@@ -35,17 +35,17 @@ def load_pass(name):
     # runs host-path chunks and the wire path, which launch smaller grids)
     big = collections.defaultdict(int)
     for r in rows:
-        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "").replace("void ", "")
         big[k] = max(big[k], int(r["Grid_Size"]))
     # persistent kernels (k_rsa_pow / k_rsa_final) launch one grid for every
     # size: keep, per kernel, the dispatches whose duration is at least half the
     # longest (the headline; the producer's public-key checks are ~4x shorter)
     dur = collections.defaultdict(dict)
     for r in rows:
-        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "").replace("void ", "")
         dur[k][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     for r in rows:
-        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("mochi::", "").replace("void ", "")
         if int(r["Grid_Size"]) != big[k] or dur[k][r["Dispatch_Id"]] < 0.5 * max(dur[k].values()):
             continue
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
