@@ -55,6 +55,14 @@ bool fixup_kernel() {
   return v;
 }
 
+bool copy_streams() {
+  static const bool v = [] {
+    const char* e = getenv("MOCHI_COPY_STREAMS");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 uint32_t default_chunk_grants() {
   const char* e = getenv("MOCHI_CHUNK_GRANTS");
   const long x = e ? atol(e) : 0;
@@ -286,6 +294,7 @@ struct mochi_ctx {
   // race on digest / perm / xbuf / decode buffers).
   hipEvent_t ev_scratch = nullptr;
   bool scratch_used = false;
+  hipStream_t scratch_st = nullptr;  // the stream ev_scratch was last recorded on
   std::vector<hipEvent_t> chunk_ev;              // host-path chunk hand-offs
   std::vector<hipEvent_t> tot_ev;                // wire host path: per-chunk decode totals on the host
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -543,10 +552,13 @@ int check_batch_host(const mochi_batch* b) {
 
 // Scratch ordering across calls and streams (see mochi_ctx::ev_scratch).
 hipError_t scratch_acquire(mochi_ctx* c, hipStream_t st) {
-  return c->scratch_used ? hipStreamWaitEvent(st, c->ev_scratch, 0) : hipSuccess;
+  // on the stream that last released the scratch, stream order already holds
+  // (a wait there is one more API call and barrier packet per small batch)
+  return c->scratch_used && c->scratch_st != st ? hipStreamWaitEvent(st, c->ev_scratch, 0) : hipSuccess;
 }
 hipError_t scratch_release(mochi_ctx* c, hipStream_t st) {
   c->scratch_used = true;
+  c->scratch_st = st;
   return hipEventRecord(c->ev_scratch, st);
 }
 
@@ -1501,12 +1513,16 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   // ONE download of the whole region -- a copy costs ~5 us of its own on the
   // GPU whatever its size, and a 2-message batch moved 5 + 7 of them.
   const bool one_copy = nch == 1 && in_total <= (4u << 20);
+  // ... and both copies on the launch stream: nothing to overlap them with, and
+  // a cross-stream hand-off is one more event record, wait and barrier packet
+  const bool on_st = one_copy && !copy_streams();  // MOCHI_COPY_STREAMS=1 (A/B): the copy streams anyway
+  hipStream_t s_in = on_st ? st : c->s_in, s_out = on_st ? st : c->s_out;
   bool pinned[7];
   for (int i = 0; i < 7; i++) pinned[i] = !one_copy && i != 3 && is_pinned(seg_src(ch[0], i));
   std::vector<mochi_write2_batch> dws(nch);
   std::vector<mochi::W2Args> args(nch);
   HIP_TRY(scratch_acquire(c, st));
-  HIP_TRY(hipEventRecord(c->ev[0], c->s_in));
+  HIP_TRY(hipEventRecord(c->ev[0], s_in));
   // phase 2 + download of chunk j (its totals must be on the host)
   auto finish = [&](size_t j) -> int {
     Chunk& k = ch[j];
@@ -1525,10 +1541,12 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     if (r) return r;
     if (dec) return MOCHI_OK;
     if (j + 1 == nch) HIP_TRY(hipEventRecord(c->ev[2], st));
-    HIP_TRY(hipEventRecord(c->chunk_ev[2 * j + 1], st));
-    HIP_TRY(hipStreamWaitEvent(c->s_out, c->chunk_ev[2 * j + 1], 0));
+    if (!on_st) {
+      HIP_TRY(hipEventRecord(c->chunk_ev[2 * j + 1], st));
+      HIP_TRY(hipStreamWaitEvent(s_out, c->chunk_ev[2 * j + 1], 0));
+    }
     auto down = [&](size_t off, size_t bytes) -> hipError_t {
-      return bytes ? hipMemcpyAsync(pout + off, dout + off, bytes, hipMemcpyDeviceToHost, c->s_out) : hipSuccess;
+      return bytes ? hipMemcpyAsync(pout + off, dout + off, bytes, hipMemcpyDeviceToHost, s_out) : hipSuccess;
     };
     if (one_copy) return (int)(down(0, out_total) == hipSuccess ? MOCHI_OK : fail(MOCHI_EHIP, "download failed"));
     const size_t no = ofo ? ofo[k.m1] - o0 : 0;
@@ -1557,10 +1575,10 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
       if (pinned[i]) src = seg_src(k, i);  // DMA'd in place (e.g. the batcher's pinned batch)
       else if (i != 3) par_memcpy(pin + k.seg[i], seg_src(k, i), n);
       if (one_copy) staged_end = k.seg[i] + n > staged_end ? k.seg[i] + n : staged_end;
-      else HIP_TRY(hipMemcpyAsync(din + k.seg[i], src, n, hipMemcpyHostToDevice, c->s_in));
+      else HIP_TRY(hipMemcpyAsync(din + k.seg[i], src, n, hipMemcpyHostToDevice, s_in));
     }
-    if (one_copy && staged_end) HIP_TRY(hipMemcpyAsync(din, pin, staged_end, hipMemcpyHostToDevice, c->s_in));
-    HIP_TRY(hipEventRecord(c->chunk_ev[2 * j], c->s_in));
+    if (one_copy && staged_end) HIP_TRY(hipMemcpyAsync(din, pin, staged_end, hipMemcpyHostToDevice, s_in));
+    if (!on_st) HIP_TRY(hipEventRecord(c->chunk_ev[2 * j], s_in));
     mochi_write2_batch& dw = dws[j];
     memset(&dw, 0, sizeof dw);
     dw.n_msgs = nm;
@@ -1572,7 +1590,7 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     dw.op_flags = ofo ? din + k.seg[4] : nullptr;
     dw.op_object_ts = seg_bytes(k, 5) ? (const int64_t*)(din + k.seg[5]) : nullptr;
     dw.expected_hash = din + k.seg[6];
-    HIP_TRY(hipStreamWaitEvent(st, c->chunk_ev[2 * j], 0));
+    if (!on_st) HIP_TRY(hipStreamWaitEvent(st, c->chunk_ev[2 * j], 0));
     if (j == 0) HIP_TRY(hipEventRecord(c->ev[1], st));
     if ((rc = w2_count(c, &dw, dout + o_status + k.m0, c->w2_cnt.as<uint32_t>() + k.cnt, tot + 4 * j, c->tot_ev[j], st,
                        &args[j])))
@@ -1623,8 +1641,8 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
     HIP_TRY(hipStreamSynchronize(st));
     return MOCHI_OK;
   }
-  HIP_TRY(hipEventRecord(c->ev[3], c->s_out));
-  HIP_TRY(hipStreamSynchronize(c->s_out));
+  HIP_TRY(hipEventRecord(c->ev[3], s_out));
+  HIP_TRY(hipStreamSynchronize(s_out));
   (void)hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[1]);
   (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);
   (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);
