@@ -297,9 +297,14 @@ struct mochi_ctx {
   hipStream_t scratch_st = nullptr;  // the stream ev_scratch was last recorded on
   std::vector<hipEvent_t> chunk_ev;              // host-path chunk hand-offs
   std::vector<hipEvent_t> tot_ev;                // wire host path: per-chunk decode totals on the host
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // two sets of the host-path call's span events: a call records into one while
+  // the other keeps the last completed call's, read only when asked
+  hipEvent_t evs[2][4] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};
+  hipEvent_t* ev = evs[0];   // the set of the call in progress
+  int ev_set = 0, ev_done = 0;  // ev's set; the last completed call's
   float last_ms[3] = {0, 0, 0};  // first upload, compute span, last download of the last host-path call
   float last_total_ms = 0;       // whole pipelined host-path call (first H2D start -> last D2H end)
+  bool timing_pending = false;   // ev[0..3] recorded, last_ms not yet read from them (resolve_timing)
   uint32_t chunk_grants = 0;     // host-path chunk target (grants), mochi_ctx_set_chunk_grants
   uint32_t small_grants = 4096;  // small-batch launch sequence up to this many grants (mochi_ctx_set_small_batch)
   // Write2 wire path: server-id table + decode scratch
@@ -443,7 +448,7 @@ mochi_ctx* mochi_ctx_create(int device, const uint8_t* moduli_be, uint32_t n_key
             hipMemcpy(c->d_keys, table.data(), sizeof(mochi::KeyEntry) * n_keys, hipMemcpyHostToDevice) == hipSuccess &&
             hipMalloc(&c->d_fold, sizeof(mochi::FoldKey) * n_keys) == hipSuccess &&
             hipMemcpy(c->d_fold, fold.data(), sizeof(mochi::FoldKey) * n_keys, hipMemcpyHostToDevice) == hipSuccess;
-  for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  for (int i = 0; i < 8 && ok; i++) ok = hipEventCreate(&c->evs[i / 4][i % 4]) == hipSuccess;
   (void)hipSetDevice(save);
   if (!ok) {
     fail(MOCHI_EHIP, "context setup failed on device %d", device);
@@ -474,8 +479,9 @@ void mochi::ctx_free(mochi_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->s_out) (void)hipStreamSynchronize(c->s_out);
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& set : c->evs)
+    for (auto& e : set)
+      if (e) (void)hipEventDestroy(e);
   for (auto& e : c->chunk_ev) (void)hipEventDestroy(e);
   for (auto& e : c->tot_ev) (void)hipEventDestroy(e);
   if (c->aux) (void)hipStreamSynchronize(c->aux);
@@ -548,6 +554,18 @@ int check_batch_host(const mochi_batch* b) {
         return fail(MOCHI_EINVAL, "MultiGrants of cert %u do not cover its grants", c);
   }
   return MOCHI_OK;
+}
+
+// The last host-path call's spans, from its events (recorded during the call,
+// read only when asked).
+void resolve_timing(mochi_ctx* c) {
+  if (!c->timing_pending) return;
+  c->timing_pending = false;
+  hipEvent_t* e = c->evs[c->ev_done];
+  (void)hipEventElapsedTime(&c->last_ms[0], e[0], e[1]);
+  (void)hipEventElapsedTime(&c->last_ms[1], e[1], e[2]);
+  (void)hipEventElapsedTime(&c->last_ms[2], e[2], e[3]);
+  (void)hipEventElapsedTime(&c->last_total_ms, e[0], e[3]);
 }
 
 // Scratch ordering across calls and streams (see mochi_ctx::ev_scratch).
@@ -824,6 +842,8 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
   uint8_t* dout = c->dev_out.as<uint8_t>();
   uint8_t* pout = (uint8_t*)c->pin_out.p;
   hipStream_t st = c->stream;
+  c->ev_set ^= 1;  // this call's span events: the other set keeps the last call's
+  c->ev = c->evs[c->ev_set];
   HIP_TRY(hipEventRecord(c->ev[0], c->s_in));
   for (size_t j = 0; j < nchunks; j++) {
     Chunk& k = ch[j];
@@ -915,10 +935,10 @@ int run_host_pipeline(mochi_ctx* c, const mochi_batch* b, const mochi_params* p,
   HIP_TRY(hipEventRecord(c->ev[3], c->s_out));
   if (hipStreamSynchronize(c->s_out) != hipSuccess)
     return fail(MOCHI_EHIP, "stream sync failed: %s", hipGetErrorString(hipGetLastError()));
-  (void)hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[1]);  // first upload (not overlapped)
-  (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);  // compute span
-  (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);  // last download (not overlapped)
-  (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
+  // first upload (not overlapped), compute span, last download (not overlapped),
+  // whole call: read from the events when asked (resolve_timing)
+  c->ev_done = c->ev_set;
+  c->timing_pending = true;
   void* dsts[] = {o->grant_flags, o->grant_ts, o->cert_accept_bits, o->cert_reason, o->cert_fail_op,
                   o->grant_valid_bits, o->op_decision, o->op_g0, o->op_ts};
   const size_t offs[] = {o_flags, o_ts, o_acc, o_reason, o_fail, o_gbits, o_dec, o_g0, o_ots};
@@ -943,8 +963,8 @@ int w2_count(mochi_ctx* c, const mochi_write2_batch* w, uint8_t* status, uint32_
              hipEvent_t ev_tot, hipStream_t st, mochi::W2Args* a) {
   const uint32_t M = w->n_msgs;
   const size_t m1 = (size_t)M + 1;
-  size_t scan_bytes = 0;
-  HIP_TRY(mochi::w2_scan_temp_bytes(M + 1, &scan_bytes));
+  size_t scan_bytes = 0;  // a small batch needs none (and the size query is ~7 host API calls)
+  if (!mochi::w2_small(M)) HIP_TRY(mochi::w2_scan_temp_bytes(M + 1, &scan_bytes));
   if (scan_bytes > c->w2_scan.cap) {
     HIP_TRY(hipStreamSynchronize(st));  // the scan scratch may be in use by an earlier chunk
     int rc = c->w2_scan.ensure(scan_bytes);
@@ -1168,6 +1188,7 @@ int mochi_ctx_set_chunk_grants(mochi_ctx* c, uint32_t grants) {
 
 int mochi_ctx_last_total_ms(mochi_ctx* c, float* total_ms) {
   if (!c || !total_ms) return fail(MOCHI_EINVAL, "null argument");
+  resolve_timing(c);
   *total_ms = c->last_total_ms;
   return MOCHI_OK;
 }
@@ -1351,9 +1372,11 @@ static int decide_fallback(mochi_ctx* c, const mochi_write2_batch* w, const moch
   v.op_decision = odec.data();
   v.op_g0 = og0.data();
   v.op_ts = ots_out.data();
+  resolve_timing(c);
   float saved[4] = {c->last_ms[0], c->last_ms[1], c->last_ms[2], c->last_total_ms};
   const int rc = run_host_pipeline(c, &b, p, &v);
   c->last_ms[0] = saved[0], c->last_ms[1] = saved[1], c->last_ms[2] = saved[2], c->last_total_ms = saved[3];
+  c->timing_pending = false;
   if (rc) return rc;
   for (size_t i = 0; i < C; i++) {
     const uint32_t m = take[i];
@@ -1522,6 +1545,8 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   std::vector<mochi_write2_batch> dws(nch);
   std::vector<mochi::W2Args> args(nch);
   HIP_TRY(scratch_acquire(c, st));
+  c->ev_set ^= 1;  // this call's span events: the other set keeps the last call's
+  c->ev = c->evs[c->ev_set];
   HIP_TRY(hipEventRecord(c->ev[0], s_in));
   // phase 2 + download of chunk j (its totals must be on the host)
   auto finish = [&](size_t j) -> int {
@@ -1643,10 +1668,8 @@ static int verify_write2_host(mochi_ctx* c, const mochi_write2_batch* w, const m
   }
   HIP_TRY(hipEventRecord(c->ev[3], s_out));
   HIP_TRY(hipStreamSynchronize(s_out));
-  (void)hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[1]);
-  (void)hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]);
-  (void)hipEventElapsedTime(&c->last_ms[2], c->ev[2], c->ev[3]);
-  (void)hipEventElapsedTime(&c->last_total_ms, c->ev[0], c->ev[3]);
+  c->ev_done = c->ev_set;
+  c->timing_pending = true;  // read from the events when asked (mochi_ctx_last_timing): four API calls off the call's path
   std::vector<uint32_t> fallback;
   for (uint32_t m = 0; m < M; m++)
     if (pout[o_status + m] == MOCHI_MSG_FALLBACK) fallback.push_back(m);
@@ -1783,6 +1806,7 @@ int mochi_ctx_read_profile(mochi_ctx* c, float* stage_ms, uint32_t n_stages, uin
 
 int mochi_ctx_last_timing(mochi_ctx* c, float* h2d_ms, float* kernels_ms, float* d2h_ms) {
   if (!c) return fail(MOCHI_EINVAL, "null ctx");
+  resolve_timing(c);
   if (h2d_ms) *h2d_ms = c->last_ms[0];
   if (kernels_ms) *kernels_ms = c->last_ms[1];
   if (d2h_ms) *d2h_ms = c->last_ms[2];

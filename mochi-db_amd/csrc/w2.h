@@ -74,6 +74,8 @@ inline size_t w2_scratch_words(uint32_t M) {
          4;  // + 4: 16-byte alignment
 }
 hipError_t w2_scan_temp_bytes(uint32_t n, size_t* bytes);
+// M messages decode without the hipcub scans (single-block kernels; no scan scratch)
+bool w2_small(uint32_t M);
 hipError_t launch_w2_count(const W2Args& a, hipStream_t stream);  // + exclusive scans
 hipError_t launch_w2_emit(const W2Args& a, hipStream_t stream);
 hipError_t launch_w2_fixup(const W2Args& a, uint32_t* accept_bits, uint8_t* reason, uint8_t* fail_op,

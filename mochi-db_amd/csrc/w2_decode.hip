@@ -1839,6 +1839,8 @@ static bool small_scan_off() {
   return off;
 }
 
+bool w2_small(uint32_t M) { return M < kW2SmallM && !small_scan_off(); }
+
 hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
   const W2Msg s = msg_view(a);
   const CE ce = ce_view(a.ce, a.ce_cap);
@@ -1846,7 +1848,7 @@ hipError_t launch_w2_count(const W2Args& a, hipStream_t st) {
   hipLaunchKernelGGL(k_w2_msg, dim3(gm1), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (a.M < kW2SmallM && !small_scan_off()) {  // the scans inside single-block kernels
+  if (w2_small(a.M)) {  // the scans inside single-block kernels
     hipLaunchKernelGGL(k_w2_entries<true>, dim3(1), dim3(1024), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce);
     if (a.M)
       hipLaunchKernelGGL(k_w2_mg, dim3(ce_blocks(a)), dim3(256), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce, a.ids,
@@ -1879,7 +1881,7 @@ hipError_t launch_w2_emit(const W2Args& a, hipStream_t st) {
           a.op_object_ts, a.op_key_off, a.op_key_len, a.mg_grant_off, a.grant_same};
   const W2Msg s = msg_view(a);
   const CE ce = ce_view(a.ce, a.ce_cap);
-  if (a.M < kW2SmallM && !small_scan_off()) {
+  if (w2_small(a.M)) {
     hipLaunchKernelGGL(k_w2_emit_small, dim3(1), dim3(1024), 0, st, a.wire, a.msg_off, a.msg_len, a.M, s, ce, a.status,
                        (const uint4*)a.off4, a.ids, a.id_off, a.n_ids, a.cert_grant_off, a.cert_op_off, a.cert_mg_off,
                        a.flags_off, a.flags_in, a.ots_in, a.N, o);
