@@ -327,12 +327,17 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final_lat(const uint32_t* __rest
   }
   __syncthreads();  // barrier 1: H and M written
   if (wv == 0) {  // t = L + 2^(28*37) (M - L - H) + 2^(28*74) H (t_hi biased) -> rows 0..147
-    uint32_t t[2 * kL];
+    // M and H read from LDS up front, all loads in flight together (read inside
+    // kara_combine's per-column scheduling fences, each waited for alone: 6.7k of
+    // a squaring's 19k cycles, MOCHI_LAT_STAMPS)
+    uint32_t t[2 * kL], hv[kL];
 #pragma unroll
     for (int k = 0; k <= kL; k++) t[kKH + k] = xr[kL + k][lane];
+#pragma unroll
+    for (int k = 0; k < kL; k++) hv[k] = xr[k][lane];
     kara_combine(
         t, [&](auto kc, uint64_t&) { return lv[decltype(kc)::value]; },
-        [&](auto kc, uint64_t&) { return xr[decltype(kc)::value][lane]; });
+        [&](auto kc, uint64_t&) { return hv[decltype(kc)::value]; });
 #pragma unroll
     for (int k = 0; k < 2 * kL; k++) xr[k][lane] = t[k];
   }
@@ -370,10 +375,13 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final_lat(const uint32_t* __rest
   // D = sum_q (h_q 2^16 + p_q) 2^(28 q), normalised (fold_reduce's carry chain)
   uint32_t x[kL];
   {
+    int pq[2 * kL];  // every pair read first: the loads in flight together, then the chain
+#pragma unroll
+    for (int i = 0; i < 2 * kL; i++) pq[i] = (int)xr[i][lane];
     int64_t carry = 0;
 #pragma unroll
     for (int q = 0; q < kL; q++) {
-      const int64_t v = mad_i64((int)xr[2 * q + 1][lane], 65536, mad_i64((int)xr[2 * q][lane], 1, carry));
+      const int64_t v = mad_i64(pq[2 * q + 1], 65536, mad_i64(pq[2 * q], 1, carry));
       x[q] = (uint32_t)v & kLimbMask;
       carry = v >> kLimbBits;
     }

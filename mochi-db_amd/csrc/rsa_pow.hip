@@ -63,9 +63,19 @@
 #ifndef MOCHI_POW_NEXT_AHEAD
 #define MOCHI_POW_NEXT_AHEAD 1  // the next group's index fetched one group ahead (below)
 #endif
+// MOCHI_LAT_STAMPS (measurement builds only): k_rsa_pow_lat's phases per wave,
+// s_memtime cycles summed over the 16 squarings -- squares, barrier 1, combine
+// (wave 0) + barrier 2, fold (+ barrier 3), barrier 4, carry chain, barrier 5,
+// whole loop -- read back with mochi_debug_lat_stamps() (scripts/lat_stamps.py)
+#ifndef MOCHI_LAT_STAMPS
+#define MOCHI_LAT_STAMPS 0
+#endif
 namespace mochi {
 #if MOCHI_POW_STAMPS
 __device__ unsigned long long g_pow_stamps[4096][5];
+#endif
+#if MOCHI_LAT_STAMPS
+__device__ unsigned long long g_lat_stamps[256][4][8];  // [block][wave][phase]
 #endif
 namespace {
 
@@ -75,6 +85,17 @@ struct Stamps {
 
 __device__ __forceinline__ uint64_t stamp() {
 #if MOCHI_POW_STAMPS
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
+}
+
+__device__ __forceinline__ uint64_t lstamp() {
+#if MOCHI_LAT_STAMPS
   __builtin_amdgcn_sched_barrier(0);
   const uint64_t t = __builtin_amdgcn_s_memtime();
   __builtin_amdgcn_sched_barrier(0);
@@ -324,9 +345,12 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
   const cptr c = as_const(a.fold[key].cadd);
   const v4i* wl = w + lane;
   const uint32_t kNoH[kHL] = {};  // nothing subtracted (k_rsa_final_lat subtracts the digest)
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t t_loop = lstamp();
 #pragma unroll 1
   for (int it = 0; it < 16; it++) {
     uint32_t lv[kL];
+    uint64_t t0 = lstamp();
 #if MOCHI_LAT_RAW  // A/B: columns as independent sums + one carry pass (measured slower: 148 vs 138 us)
     if (wv == 0) {  // L = x_lo^2, normalised, into registers
       lat_square<0>(x, lv);
@@ -367,18 +391,29 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
       });
     }
 #endif
+    uint64_t t1 = lstamp();
+    ph[0] += t1 - t0;
     __syncthreads();  // barrier 1: H and M written
+    t0 = lstamp();
+    ph[1] += t0 - t1;
     if (wv == 0) {  // t = L + 2^(28*37) (M - L - H) + 2^(28*74) H (t_hi biased) -> rows 0..147
-      uint32_t t[2 * kL];
+      // M and H read from LDS up front, all loads in flight together (read inside
+      // kara_combine's per-column scheduling fences, each waited for alone: 6.7k of
+      // a squaring's 19k cycles, MOCHI_LAT_STAMPS)
+      uint32_t t[2 * kL], hv[kL];
 #pragma unroll
       for (int k = 0; k <= kL; k++) t[kKH + k] = xr[kL + k][lane];
+#pragma unroll
+      for (int k = 0; k < kL; k++) hv[k] = xr[k][lane];
       kara_combine(
           t, [&](auto kc, uint64_t&) { return lv[decltype(kc)::value]; },
-          [&](auto kc, uint64_t&) { return xr[decltype(kc)::value][lane]; });
+          [&](auto kc, uint64_t&) { return hv[decltype(kc)::value]; });
 #pragma unroll
       for (int k = 0; k < 2 * kL; k++) xr[k][lane] = t[k];
     }
     __syncthreads();  // barrier 2: t written
+    t1 = lstamp();
+    ph[2] += t1 - t0;
     cptr ci = c;
     asm volatile("" : "+s"(ci));
     if (two) {  // each contains barrier 3
@@ -392,18 +427,37 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
       else if (wv == 2) lat_fold<2, false>(wl, ci, xr, lane, kNoH);
       else lat_fold<3, false>(wl, ci, xr, lane, kNoH);
     }
+    t0 = lstamp();
+    ph[3] += t0 - t1;
     __syncthreads();  // barrier 4: every (p, h) pair written
+    t1 = lstamp();
+    ph[4] += t1 - t0;
     if (wv < 3) {  // x' = sum_q (h_q 2^16 + p_q) 2^(28 q), normalised (fold_reduce's carry chain)
+      int pq[2 * kL];  // every pair read first: the loads in flight together, then the chain
+#pragma unroll
+      for (int i = 0; i < 2 * kL; i++) pq[i] = (int)xr[i][lane];
       int64_t carry = 0;
 #pragma unroll
       for (int q = 0; q < kL; q++) {
-        const int64_t v = mad_i64((int)xr[2 * q + 1][lane], 65536, mad_i64((int)xr[2 * q][lane], 1, carry));
+        const int64_t v = mad_i64(pq[2 * q + 1], 65536, mad_i64(pq[2 * q], 1, carry));
         x[q] = (uint32_t)v & kLimbMask;
         carry = v >> kLimbBits;
       }
     }
+    t0 = lstamp();
+    ph[5] += t0 - t1;
     __syncthreads();  // barrier 5: the pairs are read before the next H / M overwrite them
+    ph[6] += lstamp() - t0;
   }
+#if MOCHI_LAT_STAMPS
+  ph[7] = lstamp() - t_loop;
+  if (lane == 0 && blockIdx.x < 256) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) g_lat_stamps[blockIdx.x][wv][i] = ph[i];
+  }
+#else
+  (void)ph, (void)t_loop;
+#endif
   if (wv == 0 && active) {
 #pragma unroll
     for (int q = 0; q < kL; q++) a.zout[(size_t)q * a.n_slots + slot] = x[q];
@@ -416,6 +470,16 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
 extern "C" int mochi_debug_pow_stamps(unsigned long long* out, unsigned n_waves) {
   if (n_waves > 4096) n_waves = 4096;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pow_stamps), 40 * (size_t)n_waves, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#if MOCHI_LAT_STAMPS
+extern "C" int mochi_debug_lat_stamps(unsigned long long* out, unsigned n_blocks) {
+  if (n_blocks > 256) n_blocks = 256;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mochi::g_lat_stamps), 256 * (size_t)n_blocks, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -1;
 }
 #endif
 
