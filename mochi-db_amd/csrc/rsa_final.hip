@@ -307,11 +307,14 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final_lat(const uint32_t* __rest
       lv[k] = product_col<0, 0, k>(z, sv, carry);
     });
   } else if (wv == 1) {  // H = z_hi s_hi -> rows 0..73
+    uint32_t hv[kL];  // stored after the chain (k_rsa_pow_lat)
     uint64_t carry = 0;
     static_for<0, kL>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      xr[k][lane] = product_col<kKH, kKH, k>(z, sv, carry);
+      hv[k] = product_col<kKH, kKH, k>(z, sv, carry);
     });
+#pragma unroll
+    for (int k = 0; k < kL; k++) xr[k][lane] = hv[k];
   } else if (wv == 2) {  // M = (z_lo + z_hi)(s_lo + s_hi) -> rows 74..148
     uint32_t sz[kKH], ss[kKH];
 #pragma unroll
@@ -319,11 +322,14 @@ __global__ __launch_bounds__(256, 1) void k_rsa_final_lat(const uint32_t* __rest
       sz[i] = z[i] + z[kKH + i];
       ss[i] = sv[i] + sv[kKH + i];
     }
+    uint32_t mv[kL + 1];
     uint64_t carry = 0;
     static_for<0, kL + 1>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      xr[kL + k][lane] = product_col<0, 0, k>(sz, ss, carry);
+      mv[k] = product_col<0, 0, k>(sz, ss, carry);
     });
+#pragma unroll
+    for (int k = 0; k <= kL; k++) xr[kL + k][lane] = mv[k];
   }
   __syncthreads();  // barrier 1: H and M written
   if (wv == 0) {  // t = L + 2^(28*37) (M - L - H) + 2^(28*74) H (t_hi biased) -> rows 0..147

@@ -375,20 +375,27 @@ __global__ __launch_bounds__(256, 1) void k_rsa_pow_lat(const PowArgs a) {
         lv[k] = square_col<0, k>(x, carry);
       });
     } else if (wv == 1) {  // H = x_hi^2 -> rows 0..73
+      // (the limbs kept in registers and stored after the chain: stored per
+      // column, this wave's squares took 5.7k cycles against wave 0's 4.4k)
+      uint32_t hv[kL];
       uint64_t carry = 0;
       static_for<0, kL>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        xr[k][lane] = square_col<kKH, k>(x, carry);
+        hv[k] = square_col<kKH, k>(x, carry);
       });
+#pragma unroll
+      for (int k = 0; k < kL; k++) xr[k][lane] = hv[k];
     } else if (wv == 2) {  // M = (x_lo + x_hi)^2 -> rows 74..148
-      uint32_t sx[kKH];
+      uint32_t sx[kKH], mv[kL + 1];
 #pragma unroll
       for (int i = 0; i < kKH; i++) sx[i] = x[i] + x[kKH + i];
       uint64_t carry = 0;
       static_for<0, kL + 1>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        xr[kL + k][lane] = square_col<0, k>(sx, carry);
+        mv[k] = square_col<0, k>(sx, carry);
       });
+#pragma unroll
+      for (int k = 0; k <= kL; k++) xr[kL + k][lane] = mv[k];
     }
 #endif
     uint64_t t1 = lstamp();
